@@ -1,0 +1,692 @@
+// l5dh_engine.cpp -- host side of the MI355X histogram engine and the C-ABI
+// declared in include/l5dhist.h.
+//
+// One context = one GPU = one shard of the series space.  The context owns:
+//   * dense state    counts[S][1800] u32, total[S] i64, sumfix[S] i64, dirty[F]
+//   * a log of binned ingest segments (records u32[n] + tile offsets [F+1])
+//   * scratch for the per-(slab, tile) offset table and the snapshot plan
+// Ingest bins a batch immediately (count -> scans -> bin); snapshot aggregates
+// every pending segment into LDS-private tile histograms and emits summaries
+// in the same pass (the fused path) or folds into state first (range path).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/l5dhist.h"
+#include "l5dh_kernels.hpp"
+
+using namespace l5dh;
+
+namespace {
+
+// BucketedHistogram.scala:25-40 (makeLimitsFor), error 0.005.  Host copy used
+// to build the device tables; the oracle's independent restatement checks it.
+struct HostLimits {
+  int32_t L[NL];
+  bool ok = false;
+  HostLimits() {
+    const double maxValue = 2147483647.0;
+    const double factor = 1.0 + (0.005 * 2);
+    int n = 0;
+    L[n++] = 1;
+    int32_t last = -1;
+    volatile double cur = 1.0;  // volatile: no contraction / excess precision
+    for (;;) {
+      volatile double next = cur * factor;
+      if (next >= maxValue) break;
+      const int32_t v = (int32_t)next + 1;
+      if (v != last) {
+        if (n >= NL) return;
+        L[n++] = v;
+        last = v;
+      }
+      cur = next;
+    }
+    ok = (n == NL);
+  }
+};
+
+const HostLimits& host_limits() {
+  static HostLimits h;
+  return h;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct l5dh_ctx {
+  std::mutex mu;
+  int device = 0;
+  int num_cu = 256;
+  uint32_t S = 0, F = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+
+  // tables
+  int32_t* d_lim_pad = nullptr;
+  int32_t* d_mid = nullptr;
+  int32_t* d_base = nullptr;
+  // state
+  uint32_t* d_counts = nullptr;
+  int64_t* d_total = nullptr;
+  int64_t* d_sumfix = nullptr;
+  uint8_t* d_dirty = nullptr;
+  uint32_t* d_err = nullptr;
+  // scratch
+  uint32_t* d_table = nullptr;  // [G_max][F]
+  uint32_t* d_tile_tot = nullptr;
+  uint32_t* d_item_start = nullptr;
+  uint32_t* d_hot_list = nullptr;
+  uint32_t* d_header = nullptr;
+  uint32_t* h_header = nullptr;  // pinned
+  int G_max = 256;
+  // segments
+  struct Seg {
+    DevBuf recs;
+    uint32_t* tbase = nullptr;
+    size_t n = 0;
+  };
+  Seg segs[MAX_SEG];
+  int nseg = 0;
+  int max_seg = 4;
+  // staging
+  DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
+  // params
+  uint32_t cold_limit = COLD_LIMIT_MAX;
+  uint32_t hot_chunk = 1u << 20;
+  bool timing = false;
+  struct Ev {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> pending_ev;
+  std::vector<hipEvent_t> ev_pool;
+  double k_ms[L5DH_K_NKERNELS] = {0};
+  int64_t k_n[L5DH_K_NKERNELS] = {0};
+};
+
+namespace {
+
+int fail(l5dh_ctx* c, int code, const std::string& msg) {
+  c->last_error = msg;
+  return code;
+}
+
+int hipfail(l5dh_ctx* c, hipError_t e, const char* what) {
+  c->last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return -EIO;
+}
+
+#define HIPCHK(c, expr)                                \
+  do {                                                 \
+    hipError_t _e = (expr);                            \
+    if (_e != hipSuccess) return hipfail((c), _e, #expr); \
+  } while (0)
+
+hipEvent_t ev_get(l5dh_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct KTimer {
+  l5dh_ctx* c;
+  int kid;
+  hipEvent_t a = nullptr;
+  KTimer(l5dh_ctx* c_, int kid_) : c(c_), kid(kid_) {
+    if (c->timing) {
+      a = ev_get(c);
+      hipEventRecord(a, c->stream);
+    }
+  }
+  ~KTimer() {
+    if (a) {
+      hipEvent_t b = ev_get(c);
+      hipEventRecord(b, c->stream);
+      c->pending_ev.push_back({kid, a, b});
+    }
+  }
+};
+
+void collect_timing(l5dh_ctx* c) {
+  for (auto& e : c->pending_ev) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      c->k_ms[e.kid] += ms;
+      c->k_n[e.kid] += 1;
+    }
+    c->ev_pool.push_back(e.a);
+    c->ev_pool.push_back(e.b);
+  }
+  c->pending_ev.clear();
+}
+
+int sync_stream(l5dh_ctx* c) {
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  collect_timing(c);
+  return 0;
+}
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+int ensure(l5dh_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.cap >= bytes) return 0;
+  if (b.p) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t cap = std::max(bytes, (size_t)4096);
+  cap = (cap + 4095) & ~(size_t)4095;
+  hipError_t e = hipMalloc(&b.p, cap);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(c, -ENOMEM, std::string("hipMalloc staging: ") + hipGetErrorString(e));
+  }
+  b.cap = cap;
+  return 0;
+}
+
+Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base}; }
+
+State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
+
+Plan plan(l5dh_ctx* c) { return Plan{c->d_tile_tot, c->d_item_start, c->d_hot_list, c->d_header}; }
+
+Segs segs_view(l5dh_ctx* c) {
+  Segs s{};
+  s.n = c->nseg;
+  for (int j = 0; j < c->nseg; ++j) {
+    s.recs[j] = static_cast<const uint32_t*>(c->segs[j].recs.p);
+    s.tbase[j] = c->segs[j].tbase;
+  }
+  return s;
+}
+
+// Aggregate every pending segment.  final_mode: emit summaries/counts for the
+// whole series space into `out` (fused path); otherwise fold into state.
+int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
+  if (!final_mode && c->nseg == 0) return 0;
+  Segs sv = segs_view(c);
+  Plan pl = plan(c);
+  {
+    KTimer kt(c, L5DH_K_SCAN);
+    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, pl, c->stream));
+  }
+  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t items = c->h_header[0];
+  const uint32_t hot = c->h_header[1];
+  State st = state(c);
+  Tables tb = tables(c);
+  if (hot) {
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_hot_init(pl, hot, st, c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_ACCUM);
+    HIPCHK(c, launch_accum(sv, pl, items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset, c->stream));
+  }
+  if (hot) {
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, c->stream));
+  }
+  c->nseg = 0;
+  return 0;
+}
+
+int fold(l5dh_ctx* c) {
+  Outputs none{nullptr, nullptr, 0, 0};
+  return aggregate(c, 0, 0, none);
+}
+
+int check_err(l5dh_ctx* c) {
+  uint32_t e = 0;
+  HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (e) {
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
+    return fail(c, -EINVAL, "series id >= max_series in ingest batch (samples dropped)");
+  }
+  return 0;
+}
+
+int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n) {
+  if (n == 0) return 0;
+  if (n > 0xFFFFFFF0ull) return fail(c, -EINVAL, "batch larger than 2^32-16 samples");
+  if (c->nseg >= c->max_seg) {
+    int r = fold(c);
+    if (r) return r;
+  }
+  const uint32_t* ds = series;
+  const float* dv = values;
+  if (!is_device_ptr(series) || !is_device_ptr(values)) {
+    int r;
+    if ((r = ensure(c, c->stage_series, n * 4))) return r;
+    if ((r = ensure(c, c->stage_values, n * 4))) return r;
+    KTimer kt(c, L5DH_K_COPY);
+    HIPCHK(c, hipMemcpyAsync(c->stage_series.p, series, n * 4, hipMemcpyDefault, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->stage_values.p, values, n * 4, hipMemcpyDefault, c->stream));
+    ds = static_cast<const uint32_t*>(c->stage_series.p);
+    dv = static_cast<const float*>(c->stage_values.p);
+  }
+  auto& sg = c->segs[c->nseg];
+  {
+    int r = ensure(c, sg.recs, n * 4);
+    if (r) return r;
+  }
+  // slabs: one workgroup per CU at most, >= 8K samples each, 16-B aligned starts
+  int G = (int)std::min<size_t>((size_t)c->G_max, (n + 8191) / 8192);
+  if (G < 1) G = 1;
+  size_t per = (n + G - 1) / G;
+  per = (per + 3) & ~(size_t)3;
+  G = (int)((n + per - 1) / per);
+  const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
+  {
+    KTimer kt(c, L5DH_K_COUNT);
+    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, vec, c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_SCAN);
+    HIPCHK(c, launch_colscan(c->d_table, G, c->F, c->d_tile_tot, c->stream));
+    HIPCHK(c, launch_tilescan(c->d_tile_tot, c->F, sg.tbase, c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_BIN);
+    HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
+                         static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec, c->stream));
+  }
+  sg.n = n;
+  c->nseg++;
+  // No caller pointer is retained past return: wait for the batch to be binned.
+  int r = sync_stream(c);
+  if (r) return r;
+  return check_err(c);
+}
+
+bool full_range(l5dh_ctx* c, uint32_t first, uint32_t count) { return first == 0 && count == c->S; }
+
+int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {
+  if ((uint64_t)first + count > c->S) return fail(c, -EINVAL, "series range out of bounds");
+  if (count == 0) return 0;
+  int r;
+  // outputs: device pointers are written directly, host pointers via staging
+  Summary88* d_summ = nullptr;
+  int32_t* d_counts = nullptr;
+  const bool out_dev = out && is_device_ptr(out) && ((uintptr_t)out % 8 == 0);
+  const bool cnt_dev = counts_out && is_device_ptr(counts_out) && ((uintptr_t)counts_out % 8 == 0);
+  if (out) {
+    if (out_dev)
+      d_summ = reinterpret_cast<Summary88*>(out);
+    else {
+      if ((r = ensure(c, c->stage_summ, (size_t)count * 88))) return r;
+      d_summ = static_cast<Summary88*>(c->stage_summ.p);
+    }
+  }
+  if (counts_out) {
+    if (cnt_dev)
+      d_counts = counts_out;
+    else {
+      if ((r = ensure(c, c->stage_counts, (size_t)count * NB * 4))) return r;
+      d_counts = static_cast<int32_t*>(c->stage_counts.p);
+    }
+  }
+  Outputs o{d_summ, d_counts, first, count};
+  if (full_range(c, first, count)) {
+    if ((r = aggregate(c, 1, reset, o))) return r;
+  } else {
+    if ((r = fold(c))) return r;
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_rows(state(c), nullptr, nullptr, tables(c), o, reset, nullptr, c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_COPY);
+    if (out && !out_dev) HIPCHK(c, hipMemcpyAsync(out, d_summ, (size_t)count * 88, hipMemcpyDefault, c->stream));
+    if (counts_out && !cnt_dev)
+      HIPCHK(c, hipMemcpyAsync(counts_out, d_counts, (size_t)count * NB * 4, hipMemcpyDefault, c->stream));
+  }
+  return sync_stream(c);
+}
+
+}  // namespace
+
+// ============================================================================
+// C-ABI
+// ============================================================================
+extern "C" {
+
+int l5dh_abi_version(void) { return L5DH_ABI_VERSION; }
+
+const int32_t* l5dh_limits(size_t* n) {
+  const HostLimits& h = host_limits();
+  if (n) *n = h.ok ? NL : 0;
+  return h.ok ? h.L : nullptr;
+}
+
+int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  if (max_series == 0 || max_series > L5DH_MAX_SERIES) return -EINVAL;
+  if (device_mask == 0 || (device_mask & (device_mask - 1))) return -EINVAL;  // exactly one device
+  const HostLimits& hl = host_limits();
+  if (!hl.ok) return -EIO;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    return -ENODEV;
+  }
+  int dev = __builtin_ctz(device_mask);
+  if (dev >= ndev) return -ENODEV;
+  auto* c = new (std::nothrow) l5dh_ctx();
+  if (!c) return -ENOMEM;
+  c->device = dev;
+  c->S = max_series;
+  c->F = (max_series + TILE - 1) / TILE;
+  auto bail = [&](int code) {
+    l5dh_close(c);
+    return code;
+  };
+  if (hipSetDevice(dev) != hipSuccess) return bail(-EIO);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->num_cu = prop.multiProcessorCount;
+  c->G_max = std::max(1, std::min(c->num_cu, 512));
+  if (set_kernel_attributes() != hipSuccess) return bail(-EIO);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
+  c->stream = c->own_stream;
+  const size_t S = c->S, F = c->F;
+  auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
+  bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
+            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_counts, S * ROW * 4) &&
+            mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
+            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
+            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) &&
+            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16);
+  for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
+  if (!ok) {
+    (void)hipGetLastError();
+    return bail(-ENOMEM);
+  }
+  if (hipHostMalloc((void**)&c->h_header, 16, 0) != hipSuccess) return bail(-ENOMEM);
+  // constant tables
+  int32_t lim_pad[LIM_PAD], mid[NB], base[ROW] = {0};
+  for (int i = 0; i < LIM_PAD; ++i) lim_pad[i] = i < NL ? hl.L[i] : INT_MAXV;
+  for (int b = 0; b < NB; ++b) {
+    mid[b] = b == 0 ? 0 : (b >= NL ? INT_MAXV : (int32_t)(((int64_t)hl.L[b - 1] + hl.L[b]) / 2));
+    base[b] = b == 0 ? 0 : hl.L[b - 1];
+  }
+  if (hipMemcpy(c->d_lim_pad, lim_pad, sizeof(lim_pad), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
+      hipMemset(c->d_err, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return bail(-EIO);
+  *out = c;
+  return 0;
+}
+
+int l5dh_close(l5dh_ctx* c) {
+  if (!c) return -EINVAL;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto& e : c->pending_ev) {
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
+                  c->d_table, c->d_tile_tot, c->d_item_start, c->d_hot_list, c->d_header};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (auto& s : c->segs) {
+    if (s.tbase) hipFree(s.tbase);
+    if (s.recs.p) hipFree(s.recs.p);
+  }
+  DevBuf* bufs[] = {&c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
+                    &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals};
+  for (DevBuf* b : bufs)
+    if (b->p) hipFree(b->p);
+  if (c->h_header) hipHostFree(c->h_header);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return 0;
+}
+
+int l5dh_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n) {
+  if (!c) return -EINVAL;
+  if (n && (!series || !values)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  return do_ingest(c, series, values, n);
+}
+
+int l5dh_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  return do_snapshot(c, first, count, out, counts_out, reset);
+}
+
+int l5dh_export_state(l5dh_ctx* c, uint32_t first, uint32_t count, int32_t* counts, int64_t* totals, int reset) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if ((uint64_t)first + count > c->S) return fail(c, -EINVAL, "series range out of bounds");
+  if (count == 0) return 0;
+  int r;
+  if ((r = fold(c))) return r;
+  const bool cnt_dev = counts && is_device_ptr(counts) && ((uintptr_t)counts % 8 == 0);
+  const bool tot_dev = totals && is_device_ptr(totals) && ((uintptr_t)totals % 8 == 0);
+  int32_t* d_counts = nullptr;
+  int64_t* d_totals = nullptr;
+  if (counts) {
+    if (cnt_dev)
+      d_counts = counts;
+    else {
+      if ((r = ensure(c, c->stage_counts, (size_t)count * NB * 4))) return r;
+      d_counts = static_cast<int32_t*>(c->stage_counts.p);
+    }
+  }
+  if (totals) {
+    if (tot_dev)
+      d_totals = totals;
+    else {
+      if ((r = ensure(c, c->stage_totals, (size_t)count * 8))) return r;
+      d_totals = static_cast<int64_t*>(c->stage_totals.p);
+    }
+  }
+  Outputs o{nullptr, d_counts, first, count};
+  {
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_rows(state(c), nullptr, nullptr, tables(c), o, reset, d_totals, c->stream));
+  }
+  if (counts && !cnt_dev)
+    HIPCHK(c, hipMemcpyAsync(counts, d_counts, (size_t)count * NB * 4, hipMemcpyDefault, c->stream));
+  if (totals && !tot_dev) HIPCHK(c, hipMemcpyAsync(totals, d_totals, (size_t)count * 8, hipMemcpyDefault, c->stream));
+  return sync_stream(c);
+}
+
+int l5dh_summarize_dense(l5dh_ctx* c, const int32_t* counts, const int64_t* totals, size_t n, l5dh_summary* out) {
+  if (!c || (n && (!counts || !out))) return -EINVAL;
+  if (n == 0) return 0;
+  if (n > 0xFFFFFFFFull) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r;
+  const int32_t* d_counts = counts;
+  const int64_t* d_totals = totals;
+  if (!(is_device_ptr(counts) && (uintptr_t)counts % 8 == 0)) {
+    if ((r = ensure(c, c->stage_in_counts, n * NB * 4))) return r;
+    HIPCHK(c, hipMemcpyAsync(c->stage_in_counts.p, counts, n * NB * 4, hipMemcpyDefault, c->stream));
+    d_counts = static_cast<const int32_t*>(c->stage_in_counts.p);
+  }
+  if (totals && !is_device_ptr(totals)) {
+    if ((r = ensure(c, c->stage_in_totals, n * 8))) return r;
+    HIPCHK(c, hipMemcpyAsync(c->stage_in_totals.p, totals, n * 8, hipMemcpyDefault, c->stream));
+    d_totals = static_cast<const int64_t*>(c->stage_in_totals.p);
+  }
+  const bool out_dev = is_device_ptr(out) && ((uintptr_t)out % 8 == 0);
+  Summary88* d_summ;
+  if (out_dev)
+    d_summ = reinterpret_cast<Summary88*>(out);
+  else {
+    if ((r = ensure(c, c->stage_summ, n * 88))) return r;
+    d_summ = static_cast<Summary88*>(c->stage_summ.p);
+  }
+  Outputs o{d_summ, nullptr, 0, (uint32_t)n};
+  {
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_rows(state(c), d_counts, d_totals, tables(c), o, 0, nullptr, c->stream));
+  }
+  if (!out_dev) HIPCHK(c, hipMemcpyAsync(out, d_summ, n * 88, hipMemcpyDefault, c->stream));
+  return sync_stream(c);
+}
+
+int l5dh_peek(l5dh_ctx* c, uint32_t series, l5dh_bucket_count* out, size_t cap, size_t* n_out) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (series >= c->S) return fail(c, -EINVAL, "series id out of range");
+  int r;
+  if ((r = fold(c))) return r;
+  uint8_t dirty = 0;
+  std::vector<uint32_t> row(ROW, 0);
+  HIPCHK(c, hipMemcpyAsync(&dirty, c->d_dirty + (series >> TILE_SHIFT), 1, hipMemcpyDeviceToHost, c->stream));
+  if ((r = sync_stream(c))) return r;
+  if (dirty) {
+    HIPCHK(c, hipMemcpyAsync(row.data(), c->d_counts + (size_t)series * ROW, NB * 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    if ((r = sync_stream(c))) return r;
+  }
+  const HostLimits& hl = host_limits();
+  size_t k = 0;
+  for (int b = 0; b < NB; ++b) {
+    const int32_t cnt = (int32_t)row[b];
+    if (cnt > 0) {
+      if (out && k < cap) {
+        out[k].lower = b == 0 ? 0 : hl.L[b - 1];
+        out[k].upper = b < NL ? hl.L[b] : INT_MAXV;
+        out[k].count = cnt;
+      }
+      ++k;
+    }
+  }
+  if (n_out) *n_out = k;
+  return 0;
+}
+
+int l5dh_sync(l5dh_ctx* c) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r = sync_stream(c);
+  if (r) return r;
+  return check_err(c);
+}
+
+int l5dh_set_stream(l5dh_ctx* c, void* s) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r = sync_stream(c);
+  if (r) return r;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return 0;
+}
+
+int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  switch (param) {
+    case L5DH_PARAM_TIMING:
+      c->timing = v != 0;
+      return 0;
+    case L5DH_PARAM_COLD_LIMIT:
+      if (v < 0 || v > (int64_t)COLD_LIMIT_MAX) return fail(c, -EINVAL, "cold limit must be in [0, 65535]");
+      c->cold_limit = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_HOT_CHUNK:
+      if (v < 1024 || v > (1ll << 30)) return fail(c, -EINVAL, "hot chunk must be in [1024, 2^30]");
+      c->hot_chunk = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_MAX_SEGMENTS:
+      if (v < 1 || v > MAX_SEG) return fail(c, -EINVAL, "max segments must be in [1, 8]");
+      if (c->nseg > v) {
+        hipSetDevice(c->device);
+        int r = fold(c);
+        if (r) return r;
+      }
+      c->max_seg = (int)v;
+      return 0;
+    default:
+      return fail(c, -EINVAL, "unknown parameter");
+  }
+}
+
+int l5dh_kernel_time(l5dh_ctx* c, int kid, double* ms, int64_t* launches, int reset_after) {
+  if (!c || kid < 0 || kid >= L5DH_K_NKERNELS) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r = sync_stream(c);
+  if (r) return r;
+  if (ms) *ms = c->k_ms[kid];
+  if (launches) *launches = c->k_n[kid];
+  if (reset_after) {
+    c->k_ms[kid] = 0;
+    c->k_n[kid] = 0;
+  }
+  return 0;
+}
+
+int l5dh_device(l5dh_ctx* c, int* dev) {
+  if (!c || !dev) return -EINVAL;
+  *dev = c->device;
+  return 0;
+}
+
+uint32_t l5dh_max_series(l5dh_ctx* c) { return c ? c->S : 0; }
+
+int l5dh_pin_alloc(size_t bytes, void** out) {
+  if (!out || bytes == 0) return -EINVAL;
+  if (hipHostMalloc(out, bytes, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return -ENOMEM;
+  }
+  return 0;
+}
+
+int l5dh_pin_free(void* p) {
+  if (!p) return -EINVAL;
+  return hipHostFree(p) == hipSuccess ? 0 : -EINVAL;
+}
+
+const char* l5dh_last_error(l5dh_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// l5dh_kernels.hpp -- device-side layout constants and host launchers for the
+// MI355X histogram engine.  See DESIGN.md for the data layout in HBM.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace l5dh {
+
+constexpr int NL = 1797;            // BucketedHistogram.scala:42
+constexpr int NB = 1798;            // counts = limits + overflow bucket
+constexpr int INT_MAXV = 2147483647;
+constexpr int LIM_PAD = 2048;       // limits padded with Int.MaxValue for an 11-step search
+constexpr int TILE = 32;            // series per tile (unit of LDS privatization)
+constexpr int TILE_SHIFT = 5;
+constexpr int ROW = 1800;           // state row stride in u32 (16-B aligned rows)
+constexpr int CROW = 900;           // u16-packed cold row in LDS, in u32 words
+constexpr int HROW = 1800;          // u32 hot row in LDS
+constexpr uint32_t OFF_ESC = 0xFFFFu;
+constexpr int MAX_SEG = 8;
+constexpr int WG = 1024;            // threads per workgroup of the heavy kernels
+constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow below this
+
+// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows (hot)
+constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + 16 * 8 + 64;
+
+struct Tables {            // constant tables in HBM (7-8 KB each, L2 resident)
+  const int32_t* lim_pad;  // [2048]
+  const int32_t* mid;      // [1798] value reported for bucket b
+  const int32_t* base;     // [1798] lower limit of bucket b (0 for b == 0)
+};
+
+struct Segs {              // binned ingest batches awaiting aggregation
+  const uint32_t* recs[MAX_SEG];
+  const uint32_t* tbase[MAX_SEG];  // [F+1] record offset of each tile
+  int n;
+};
+
+struct Summary88 {
+  int64_t count, min, max, sum, p50, p90, p95, p99, p9990, p9999;
+  double avg;
+};
+static_assert(sizeof(Summary88) == 88, "HistogramSummary layout");
+
+struct State {
+  uint32_t* counts;        // [S][ROW]
+  int64_t* total;          // [S]
+  int64_t* sumfix;         // [S] exact sum corrections from escaped records
+  uint8_t* dirty;          // [F] tile holds live counts in `counts`
+  uint32_t S, F;
+};
+
+struct Plan {
+  uint32_t* tile_tot;      // [F]
+  uint32_t* item_start;    // [F+1]
+  uint32_t* hot_list;      // [F]
+  uint32_t* header;        // [4] total items, hot tiles
+};
+
+struct Outputs {
+  Summary88* summ;         // nullable, index = series - first
+  int32_t* counts;         // nullable, [count][1798]
+  uint32_t first, count;
+};
+
+// ---- launchers (all enqueue on `st`) ----
+hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
+                        uint32_t* table, uint32_t* err, bool vec, hipStream_t st);
+hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* tile_tot, hipStream_t st);
+hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_base, hipStream_t st);
+hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
+                      uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
+                      int64_t* sumfix, bool vec, hipStream_t st);
+hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
+                       hipStream_t st);
+hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st);
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t num_items, State state, Tables tb, Outputs out,
+                        uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset, hipStream_t st);
+hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
+                             int reset, hipStream_t st);
+// Summaries of state rows [first, first+count) (ext == nullptr) or of external
+// dense rows ext[count][1798] + ext_total[count].
+hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out,
+                       int reset, int64_t* totals_out, hipStream_t st);
+hipError_t set_kernel_attributes();
+
+}  // namespace l5dh

@@ -1,0 +1,212 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Bucket counts, count/sum/min/max/percentiles are compared bit-exactly; avg is
+compared bit-exactly as well (sum and count are exact integers on both sides, so
+IEEE division gives the same double; BASELINE allows 1e-12 relative).
+"""
+import numpy as np
+import pytest
+
+from linkerd_amd import synth
+from linkerd_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+EDGE_VALUES = np.array([
+    0.0, 0.25, 0.5, 0.999, 1.0, 1.5, 2.0, 99.9, 100.0, 112.0, 112.99, 113.0, 114.0, 115.0, 116.5,
+    3030.0, 2323.0, 65535.0, 65536.0, 1e6, 6.5e6, 1.3e7, 1e9, 2137204090.0, 2137204091.0,
+    2147483520.0, 2147483648.0, 3e9, 1e20, np.inf,
+    -0.0, -0.5, -1.0, -113.0, -3e9, -5e9, -1e19, -np.inf, np.nan,
+], dtype=np.float32)
+
+
+def _engine(S):
+    from linkerd_amd.engine import HistogramEngine
+    return HistogramEngine(S)
+
+
+def _assert_summaries_equal(got, want, label=""):
+    for f in N.SUMMARY_FIELDS:
+        g, w = got[f], want[f]
+        if f == "avg":
+            bad = ~((g == w) | (np.isnan(g) & np.isnan(w)))
+        else:
+            bad = g != w
+        if bad.any():
+            i = int(np.flatnonzero(bad)[0])
+            raise AssertionError(f"{label} field {f}: {int(bad.sum())} mismatches; first series {i}: "
+                                 f"got {g[i]!r} want {w[i]!r}\n got={got[i]}\nwant={want[i]}")
+
+
+def _random_batch(rng, S, n, edge_frac=0.01):
+    series = rng.integers(0, S, size=n, dtype=np.uint32)
+    mu = np.log(rng.uniform(1, 1000, size=S))
+    vals = np.exp(mu[series] + 0.8 * rng.standard_normal(n)).astype(np.float32)
+    k = int(n * edge_frac)
+    if k:
+        pos = rng.choice(n, size=k, replace=False)
+        vals[pos] = rng.choice(EDGE_VALUES, size=k)
+    return series, vals
+
+
+def test_limits_match_oracle(oracle):
+    np.testing.assert_array_equal(N.limits(), oracle.limits())
+
+
+def test_small_random_bitexact(oracle):
+    rng = np.random.default_rng(11)
+    S, n = 1000, 300_000
+    series, vals = _random_batch(rng, S, n)
+    eng = _engine(S)
+    eng.ingest(series, vals)
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals)
+    np.testing.assert_array_equal(counts, o.counts())
+    want = o.snapshot(reset=True)
+    _assert_summaries_equal(got, want, "small")
+    # after reset everything is empty
+    got2 = eng.snapshot(reset=True)
+    assert (got2["count"] == 0).all() and (got2["sum"] == 0).all() and (got2["avg"] == 0).all()
+
+
+def test_edge_values_every_series(oracle):
+    S = 70  # not a multiple of the 32-series tile
+    series = np.repeat(np.arange(S, dtype=np.uint32), EDGE_VALUES.size)
+    vals = np.tile(EDGE_VALUES, S)
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(series.size)
+    series, vals = series[perm], vals[perm]
+    eng = _engine(S)
+    eng.ingest(series, vals)
+    got, counts = eng.snapshot(with_counts=True)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(), "edge")
+
+
+@pytest.mark.parametrize("reset", [False, True])
+def test_multi_batch_and_cumulative_snapshots(oracle, reset):
+    """Several ingests (segments + folds) and snapshots with / without reset
+    (Prometheus P2 is cumulative: snapshot() without reset, PrometheusTelemeterTest.scala:70-86)."""
+    rng = np.random.default_rng(5 + reset)
+    S = 333
+    eng = _engine(S)
+    eng.set_param(N.PARAM_MAX_SEGMENTS, 2)
+    o = oracle.OracleHistograms(S)
+    for it in range(3):
+        for b in range(3):
+            series, vals = _random_batch(rng, S, int(rng.integers(1, 20000)))
+            eng.ingest(series, vals)
+            o.ingest(series, vals)
+        got, counts = eng.snapshot(reset=reset, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"iter {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=reset), f"iter {it}")
+
+
+def test_hot_tile_split_path(oracle):
+    """Force the split (hot-tile) path: small cold limit and chunk."""
+    rng = np.random.default_rng(9)
+    S = 100
+    eng = _engine(S)
+    eng.set_param(N.PARAM_COLD_LIMIT, 500)
+    eng.set_param(N.PARAM_HOT_CHUNK, 1024)
+    o = oracle.OracleHistograms(S)
+    # skewed: series 0..3 hot
+    series = np.concatenate([rng.integers(0, 4, 40000), rng.integers(0, S, 5000)]).astype(np.uint32)
+    vals = np.exp(3 + rng.standard_normal(series.size)).astype(np.float32)
+    vals[::97] = rng.choice(EDGE_VALUES, size=vals[::97].size)
+    eng.ingest(series, vals)
+    o.ingest(series, vals)
+    got, counts = eng.snapshot(reset=False, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(reset=False), "hot1")
+    # second round on top of dirty state, then reset
+    eng.ingest(series[:30000], vals[:30000])
+    o.ingest(series[:30000], vals[:30000])
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(reset=True), "hot2")
+
+
+def test_range_snapshot_peek_export(oracle):
+    rng = np.random.default_rng(21)
+    S = 500
+    series, vals = _random_batch(rng, S, 100_000)
+    eng = _engine(S)
+    eng.ingest(series, vals)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals)
+    want_all = o.snapshot(reset=False)
+    got = eng.snapshot(first=100, count=50, reset=True)
+    _assert_summaries_equal(got, want_all[100:150], "range")
+    # reset only that range
+    got_all = eng.snapshot(reset=False)
+    want_after = want_all.copy()
+    want_after[100:150] = np.zeros(50, dtype=want_after.dtype)
+    _assert_summaries_equal(got_all, want_after, "after range reset")
+    # peek == bucketAndCounts of the oracle
+    L = oracle.limits()
+    for s in (0, 7, 499):
+        pk = eng.peek(s)
+        c = o.counts()[s]
+        nz = np.flatnonzero(c > 0)
+        assert pk.size == nz.size
+        np.testing.assert_array_equal(pk["count"], c[nz])
+        np.testing.assert_array_equal(pk["lower"], np.where(nz == 0, 0, L[np.maximum(nz - 1, 0)]))
+        np.testing.assert_array_equal(pk["upper"], np.where(nz < 1797, L[np.minimum(nz, 1796)], 2147483647))
+    counts, totals = eng.export_state()
+    want_counts = o.counts()
+    want_counts[100:150] = 0
+    np.testing.assert_array_equal(counts, want_counts)
+    want_tot = o.totals()
+    want_tot[100:150] = 0
+    np.testing.assert_array_equal(totals, want_tot)
+    summ = eng.summarize_dense(counts, totals)
+    _assert_summaries_equal(summ, want_after, "summarize_dense")
+
+
+def test_invalid_series_reported(oracle):
+    S = 64
+    eng = _engine(S)
+    series = np.array([1, 2, 64, 3, 1000], dtype=np.uint32)
+    vals = np.array([1, 2, 3, 4, 5], dtype=np.float32)
+    with pytest.raises(N.L5dhError):
+        eng.ingest(series, vals)
+    got = eng.snapshot()
+    o = oracle.OracleHistograms(S)
+    o.ingest(series[[0, 1, 3]], vals[[0, 1, 3]])
+    _assert_summaries_equal(got, o.snapshot(), "invalid dropped")
+
+
+def test_c2_slice_bitexact(oracle):
+    """C2 recipe at 1/10 of the series: 10k series x 1k samples."""
+    series, vals = synth.c2(S=10_000, K=1_000)
+    eng = _engine(10_000)
+    eng.ingest(series, vals)
+    got, counts = eng.snapshot(with_counts=True)
+    o = oracle.OracleHistograms(10_000)
+    o.ingest(series, vals, threads=8)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(), "c2 slice")
+
+
+def test_device_buffers_in_and_out(oracle):
+    import torch
+    rng = np.random.default_rng(4)
+    S = 2000
+    series, vals = _random_batch(rng, S, 500_000)
+    eng = _engine(S)
+    ds = torch.from_numpy(series.view(np.int32)).cuda()
+    dv = torch.from_numpy(vals).cuda()
+    eng.ingest(ds, dv)
+    summ = torch.zeros(S * 11, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros((S, 1798), dtype=torch.int32, device="cuda")
+    eng.snapshot_into(summ, cnt)
+    torch.cuda.synchronize()
+    got = summ.cpu().numpy().view(N.SUMMARY_DTYPE)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), o.counts())
+    _assert_summaries_equal(got, o.snapshot(), "device io")
