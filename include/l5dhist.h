@@ -66,18 +66,20 @@ enum {
   L5DH_PARAM_TIMING = 1,      /* 1: record HIP events around every kernel launch */
   L5DH_PARAM_COLD_LIMIT = 2,  /* max records for the single-pass tile path (<= 65535) */
   L5DH_PARAM_HOT_CHUNK = 3,   /* records per work item on the split (hot-tile) path */
-  L5DH_PARAM_MAX_SEGMENTS = 4 /* binned ingest batches kept before folding (1..8) */
+  L5DH_PARAM_MAX_SEGMENTS = 4, /* binned ingest batches kept before folding (1..8) */
+  L5DH_PARAM_BIN_MODE = 5      /* 0 auto, 1 single-level scatter, 2 two-level partition */
 };
 
 /* Kernel ids for l5dh_kernel_time */
 enum {
   L5DH_K_COUNT = 0,  /* per-slab tile histogram of the batch */
   L5DH_K_SCAN = 1,   /* slab/tile offset scans and the snapshot plan */
-  L5DH_K_BIN = 2,    /* bucketize (LDS binary search) + scatter records by tile */
+  L5DH_K_BIN = 2,    /* level-1 partition by super-tile (or the single-level bin) */
   L5DH_K_ACCUM = 3,  /* LDS-private tile histograms + fused summary / dense flush */
   L5DH_K_HOT = 4,    /* split-tile init/finish and row summaries */
   L5DH_K_COPY = 5,   /* H2D/D2H staging copies */
-  L5DH_K_NKERNELS = 6
+  L5DH_K_BIN2 = 6,   /* level-2 partition + bucketize (LUT-bracketed search) */
+  L5DH_K_NKERNELS = 7
 };
 
 /* Reference: BucketedHistogram() per Stat (MetricsTree.scala:88).  Opens a
@@ -92,8 +94,9 @@ const int32_t* l5dh_limits(size_t* n);
 
 /* Reference: Metric.Stat.add(Float) (Metric.scala:30-33), batched: adds
  * values[i] to series series[i] for i < n.  Integer-only effect, so order
- * independent.  Out-of-range ids are dropped and reported as -EINVAL by the
- * next l5dh_snapshot / l5dh_sync. */
+ * independent.  Samples with out-of-range ids are dropped and the call
+ * returns -EINVAL after ingesting the valid ones.  Returns once the batch is
+ * binned on the device (no caller pointer is retained). */
 int l5dh_ingest(l5dh_ctx* ctx, const uint32_t* series, const float* values, size_t n);
 
 /* Reference: Metric.Stat.snapshot() + reset() per Stat as driven by

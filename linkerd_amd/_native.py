@@ -29,9 +29,10 @@ PARAM_TIMING = 1
 PARAM_COLD_LIMIT = 2
 PARAM_HOT_CHUNK = 3
 PARAM_MAX_SEGMENTS = 4
+PARAM_BIN_MODE = 5
 
-K_COUNT, K_SCAN, K_BIN, K_ACCUM, K_HOT, K_COPY = range(6)
-KERNEL_NAMES = ("count", "scan", "bin", "accum", "hot", "copy")
+K_COUNT, K_SCAN, K_BIN, K_ACCUM, K_HOT, K_COPY, K_BIN2 = range(7)
+KERNEL_NAMES = ("count", "scan", "bin1", "accum", "hot", "copy", "bin2")
 
 
 class NativeLibraryMissing(ImportError):

@@ -1,0 +1,308 @@
+// l5dh_device.hpp -- device helpers shared by the ingest and snapshot kernels:
+// Java numerics, the bucket search, block/wave scans and the wave-cooperative
+// HistogramSummary.  Semantics restated from (reference paths relative to the
+// linkerd checkout):
+//   Metric.Stat.add(Float) -> BucketedHistogram.add(Long)   Metric.scala:30-33
+//   Metric.Stat.summary / HistogramSummary                  Metric.scala:53-67,76-88
+//   limits                                                  BucketedHistogram.scala:25-46
+// and finagle-stats 6.45.0 BucketedHistogram (percentile/min/max/average), as
+// written out in SURVEY.md §8a.
+#pragma once
+
+#include "l5dh_kernels.hpp"
+
+namespace l5dh {
+namespace {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Java (long) float conversion (JLS 5.1.3), Metric.scala:32 `value.toLong`.
+__device__ __forceinline__ int64_t java_f2l(float f) {
+  if (f != f) return 0;
+  if (f >= 9.223372036854775808e18f) return INT64_MAX;
+  if (f <= -9.223372036854775808e18f) return INT64_MIN;
+  return (int64_t)f;
+}
+
+// java.lang.Math.round for 0 <= x < 2^52: floor(x) + (frac >= 0.5), exact.
+__device__ __forceinline__ int64_t java_round_nonneg(double x) {
+  double fl = floor(x);
+  double fr = __dsub_rn(x, fl);
+  return (int64_t)fl + (fr >= 0.5 ? 1 : 0);
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// ---- bin groups ----------------------------------------------------------
+// Lane l of a wave owns bins [28l, 28l+28) = groups q = 0..6 of 4 bins; lane 63
+// also owns 1792..1797 (groups 7 and 8; group 8 = bins 1796, 1797 + padding).
+__device__ __forceinline__ int lane_groups(int lane) { return lane == 63 ? 9 : 7; }
+
+// Count sources: get4(b0) returns bins b0..b0+3 (b0 % 4 == 0); bins >= 1798 read 0.
+struct SrcLds16 {  // u16-packed row in LDS (cold tile: counts of the new records)
+  const uint32_t* row;
+  __device__ __forceinline__ uint4 get4(int b0) const {
+    const uint2 w = *reinterpret_cast<const uint2*>(row + (b0 >> 1));  // word 899 is zero padding
+    return make_uint4(w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16);
+  }
+};
+struct SrcRow32 {  // state row, stride ROW = 1800 u32, 16-B aligned
+  const uint32_t* row;
+  __device__ __forceinline__ uint4 get4(int b0) const {
+    uint4 v = *reinterpret_cast<const uint4*>(row + b0);
+    if (b0 == 1796) v.z = v.w = 0u;
+    return v;
+  }
+};
+struct SrcExt {  // external dense rows, stride 1798 int32 (8-B aligned)
+  const int32_t* row;
+  __device__ __forceinline__ uint4 get4(int b0) const {
+    const uint2 a = *reinterpret_cast<const uint2*>(row + b0);
+    uint2 b = make_uint2(0u, 0u);
+    if (b0 != 1796) b = *reinterpret_cast<const uint2*>(row + b0 + 2);
+    return make_uint4(a.x, a.y, b.x, b.y);
+  }
+};
+
+__device__ __forceinline__ uint32_t sum4(uint4 v) { return v.x + v.y + v.z + v.w; }
+
+__device__ __forceinline__ uint64_t dot4(uint4 v, const int32_t* __restrict__ base, int b0) {
+  const uint4 bb = *reinterpret_cast<const uint4*>(base + b0);  // base table padded to 1800 with 0
+  return (uint64_t)v.x * bb.x + (uint64_t)v.y * bb.y + (uint64_t)v.z * bb.z + (uint64_t)v.w * bb.w;
+}
+
+__device__ __forceinline__ void store4_1798(int32_t* __restrict__ row, int b0, uint4 v) {
+  *reinterpret_cast<uint2*>(row + b0) = make_uint2(v.x, v.y);
+  if (b0 != 1796) *reinterpret_cast<uint2*>(row + b0 + 2) = make_uint2(v.z, v.w);
+}
+
+__device__ __forceinline__ void store4_state(uint32_t* __restrict__ row, int b0, uint4 v) {
+  *reinterpret_cast<uint4*>(row + b0) = v;
+}
+
+// Wave-cooperative summary of one series (Metric.Stat.summary, Metric.scala:53-67;
+// upstream percentile/minimum/maximum/average).  g[q] = sum of the lane's group q.
+//   min  = first bucket whose running count >= 1
+//   pXX  = first bucket whose running count >= Math.round(p * num)
+//   max  = first bucket whose running count >= num (= last non-empty bucket)
+// each reported as the bucket midpoint (mid[0] = 0, mid[1797] = Int.MaxValue).
+// The owner lane of each of the 8 targets is found by ballot over the lane
+// prefix; lanes 0..7 then locate the group (shuffles) and the bin (one get4).
+template <class Src>
+__device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& src, int64_t total,
+                                             const int32_t* __restrict__ mid, Summary88* __restrict__ out) {
+  const int lane = lane_id();
+  uint64_t ls = 0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) ls += g[q];
+  const uint64_t incl = wave_incl_scan(ls);
+  const uint64_t excl = incl - ls;
+  const uint64_t num = __shfl(incl, 63, 64);
+  const double dn = (double)num;
+
+  int my_owner = 0;
+  uint64_t my_t = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint64_t t;
+    if (k == 0)
+      t = num ? 1 : 0;
+    else if (k == 7)
+      t = num;
+    else {
+      const double p = k == 1 ? 0.50 : k == 2 ? 0.90 : k == 3 ? 0.95 : k == 4 ? 0.99 : k == 5 ? 0.999 : 0.9999;
+      t = (uint64_t)java_round_nonneg(__dmul_rn(p, dn));
+    }
+    const unsigned long long m = __ballot(t != 0 && excl < t && t <= incl);
+    const int owner = m ? (__ffsll((long long)m) - 1) : 0;
+    if (lane == k) {
+      my_owner = owner;
+      my_t = t;
+    }
+  }
+  uint64_t acc = __shfl(excl, my_owner, 64);
+  int qsel = 0;
+  bool done = false;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const uint32_t gq = __shfl(g[q], my_owner, 64);
+    if (!done) {
+      if (acc + gq >= my_t) {
+        qsel = q;
+        done = true;
+      } else {
+        acc += gq;
+      }
+    }
+  }
+  int64_t res = 0;
+  if (lane < 8 && my_t != 0) {
+    const int b0 = 28 * my_owner + 4 * qsel;
+    const uint4 v = src.get4(b0);
+    int b = b0 + 3;
+    if (acc + v.x >= my_t)
+      b = b0;
+    else if (acc + v.x + v.y >= my_t)
+      b = b0 + 1;
+    else if (acc + v.x + v.y + v.z >= my_t)
+      b = b0 + 2;
+    res = mid[b];
+  }
+  // field f of HistogramSummary: count, min(k0), max(k7), sum, p50..p9999(k1..k6), avg
+  const int f = lane;
+  const int srcl = (f == 1) ? 0 : (f == 2) ? 7 : (f >= 4 && f <= 9) ? (f - 3) : 0;
+  const int64_t r = __shfl(res, srcl, 64);
+  if (out != nullptr && f < 11) {
+    int64_t val;
+    if (f == 0)
+      val = (int64_t)num;
+    else if (f == 3)
+      val = total;
+    else if (f == 10) {
+      const double avg = num == 0 ? 0.0 : __ddiv_rn((double)total, dn);
+      val = __double_as_longlong(avg);
+    } else
+      val = r;
+    reinterpret_cast<int64_t*>(out)[f] = val;
+  }
+}
+
+constexpr int NB4 = 450;  // groups of 4 bins covering 1798 bins (+2 padding)
+
+// Pass over a row source: optional dense copy in a coalesced lane order (lane l
+// copies groups l, l+64, ...), then the blocked group sums of the summary.
+template <class Src>
+__device__ __forceinline__ void row_pass(const Src& src, uint32_t (&g)[9], int32_t* __restrict__ out_row) {
+  const int lane = lane_id();
+  if (out_row) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = lane + 64 * k;
+      if (q < NB4) store4_1798(out_row, 4 * q, src.get4(4 * q));
+    }
+  }
+  const int ng = lane_groups(lane);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(src.get4(28 * lane + 4 * q)) : 0u;
+}
+
+template <int NT = 1024>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds /*[NT/64+1]*/, uint32_t* total) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) lds[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < NW; ++k) {
+      const uint32_t q = lds[k];
+      lds[k] = acc;
+      acc += q;
+    }
+    lds[NW] = acc;
+  }
+  __syncthreads();
+  const uint32_t r = lds[w] + x - v;
+  if (total) *total = lds[NW];
+  __syncthreads();
+  return r;
+}
+
+
+// Bucket of a non-negative key v < Int.MaxValue, bit-identical to
+// upper_bound(limits, v) (== the Arrays.binarySearch insertion rule of
+// BucketedHistogram.add): a 1664-entry LUT indexed by the exponent and the top
+// 6 mantissa bits of v brackets the bucket from below; each LUT interval
+// contains at most two limits (checked exhaustively on the host when the
+// table is built), so two compares against the LDS limits finish the search.
+__device__ __forceinline__ uint32_t bucket_lut(uint32_t v, const uint16_t* __restrict__ lut,
+                                               const int32_t* __restrict__ lim) {
+  uint32_t idx;
+  if (v < 64u) {
+    idx = v;
+  } else {
+    const int e = 31 - __clz((int)v);
+    idx = 64u + (uint32_t)(e - 6) * 64u + ((v >> (e - 6)) & 63u);
+  }
+  uint32_t b = lut[idx];
+  b += (lim[b] <= (int32_t)v) ? 1u : 0u;
+  b += (lim[b] <= (int32_t)v) ? 1u : 0u;
+  return b;
+}
+
+// Full 11-step search for any int32 key (negative keys come from the Long.toInt
+// wrap of negative samples; rare path).
+__device__ __forceinline__ uint32_t search_key(int32_t key, const int32_t* __restrict__ lim) {
+  int idx = 0;
+#pragma unroll
+  for (int step = 1024; step > 0; step >>= 1)
+    if (lim[idx + step - 1] <= key) idx += step;
+  return (uint32_t)(idx < NL ? idx : NL);
+}
+
+// upstream BucketedHistogram.add(Long) applied to Metric.Stat.add's
+// `value.toLong` (Metric.scala:32): returns the bucket and the sample's
+// contribution to `total` (Int.MaxValue for the overflow bucket).
+__device__ __forceinline__ uint32_t bucketize(float f, const uint16_t* __restrict__ lut,
+                                              const int32_t* __restrict__ lim, int64_t& contrib) {
+  if (f >= 0.0f && f < 2147483648.0f) {  // common case: v in [0, 2147483520]
+    const uint32_t v = (uint32_t)f;
+    contrib = v;
+    return bucket_lut(v, lut, lim);
+  }
+  const int64_t v = java_f2l(f);
+  if (v >= (int64_t)INT_MAXV) {
+    contrib = INT_MAXV;
+    return NL;
+  }
+  contrib = v;
+  const int32_t key = (int32_t)(uint32_t)(uint64_t)v;  // Long.toInt: low 32 bits
+  return (key >= 0 && key < INT_MAXV) ? bucket_lut((uint32_t)key, lut, lim) : search_key(key, lim);
+}
+
+// Visit records r[a, e) with 16-B loads, two in flight per thread per step.
+template <int NT, class Fn>
+__device__ __forceinline__ void for_records(const uint32_t* __restrict__ r, uint32_t a, uint32_t e, Fn&& fn) {
+  if (a >= e) return;
+  const uint32_t a4 = min(e, (a + 3u) & ~3u);
+  if (threadIdx.x < a4 - a) fn(r[a + threadIdx.x]);
+  const uint4* __restrict__ p = reinterpret_cast<const uint4*>(r + a4);
+  const uint32_t nv = (e - a4) >> 2;
+  uint32_t i = threadIdx.x;
+  for (; i + NT < nv; i += 2 * NT) {
+    const uint4 x = p[i];
+    const uint4 y = p[i + NT];
+    fn(x.x); fn(x.y); fn(x.z); fn(x.w);
+    fn(y.x); fn(y.y); fn(y.z); fn(y.w);
+  }
+  if (i < nv) {
+    const uint4 x = p[i];
+    fn(x.x); fn(x.y); fn(x.z); fn(x.w);
+  }
+  const uint32_t t0 = a4 + (nv << 2);
+  if (t0 + threadIdx.x < e) fn(r[t0 + threadIdx.x]);
+}
+
+}  // namespace
+}  // namespace l5dh

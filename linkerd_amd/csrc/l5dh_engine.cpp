@@ -65,6 +65,33 @@ struct DevBuf {
 
 }  // namespace
 
+namespace l5dh {
+// bucket(v) = number of limits <= v (upper bound), for the LUT builder.
+static int host_bucket(const int32_t* L, int64_t v) {
+  int lo = 0, hi = NL;
+  while (lo < hi) {
+    const int m = (lo + hi) / 2;
+    if ((int64_t)L[m] <= v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+int build_bucket_lut(const int32_t* L, uint16_t* lut) {
+  int maxin = 0, k = 0;
+  for (int v = 0; v < 64; ++v) lut[k++] = (uint16_t)host_bucket(L, v);
+  for (int e = 6; e <= 30; ++e)
+    for (int m = 0; m < 64; ++m) {
+      const int64_t start = (int64_t)(64 + m) << (e - 6);
+      int64_t end = ((int64_t)(64 + m + 1) << (e - 6)) - 1;
+      if (end > 2147483646) end = 2147483646;
+      const int b0 = host_bucket(L, start);
+      lut[k++] = (uint16_t)b0;
+      maxin = std::max(maxin, host_bucket(L, end) - b0);
+    }
+  return k == LUT_N ? maxin : 99;
+}
+}  // namespace l5dh
+
 struct l5dh_ctx {
   std::mutex mu;
   int device = 0;
@@ -78,6 +105,7 @@ struct l5dh_ctx {
   int32_t* d_lim_pad = nullptr;
   int32_t* d_mid = nullptr;
   int32_t* d_base = nullptr;
+  uint16_t* d_lut = nullptr;
   // state
   uint32_t* d_counts = nullptr;
   int64_t* d_total = nullptr;
@@ -102,6 +130,8 @@ struct l5dh_ctx {
   int nseg = 0;
   int max_seg = 4;
   // staging
+  DevBuf scratch1;  // level-1 records of the two-level partition
+  int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
@@ -214,7 +244,7 @@ int ensure(l5dh_ctx* c, DevBuf& b, size_t bytes) {
   return 0;
 }
 
-Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base}; }
+Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c->d_lut}; }
 
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
@@ -318,7 +348,19 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     HIPCHK(c, launch_colscan(c->d_table, G, c->F, c->d_tile_tot, c->stream));
     HIPCHK(c, launch_tilescan(c->d_tile_tot, c->F, sg.tbase, c->stream));
   }
-  {
+  const bool two_level = c->bin_mode != 1;
+  if (two_level) {
+    int r = ensure(c, c->scratch1, n * 4);
+    if (r) return r;
+    {
+      KTimer kt(c, L5DH_K_BIN);
+      HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
+                            static_cast<uint32_t*>(c->scratch1.p), c->d_sumfix, vec, c->stream));
+    }
+    KTimer kt(c, L5DH_K_BIN2);
+    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), G, c->F, c->d_table, c->d_tile_tot, sg.tbase,
+                          tables(c), static_cast<uint32_t*>(sg.recs.p), c->stream));
+  } else {
     KTimer kt(c, L5DH_K_BIN);
     HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
                          static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec, c->stream));
@@ -416,14 +458,14 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   if (hipSetDevice(dev) != hipSuccess) return bail(-EIO);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->num_cu = prop.multiProcessorCount;
-  c->G_max = std::max(1, std::min(c->num_cu, 512));
-  if (set_kernel_attributes() != hipSuccess) return bail(-EIO);
+  c->G_max = std::max(1, std::min(2 * c->num_cu, 512));
+  if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   c->stream = c->own_stream;
   const size_t S = c->S, F = c->F;
   auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
-            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_counts, S * ROW * 4) &&
+            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 2) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
             mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) &&
@@ -441,7 +483,10 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
     mid[b] = b == 0 ? 0 : (b >= NL ? INT_MAXV : (int32_t)(((int64_t)hl.L[b - 1] + hl.L[b]) / 2));
     base[b] = b == 0 ? 0 : hl.L[b - 1];
   }
-  if (hipMemcpy(c->d_lim_pad, lim_pad, sizeof(lim_pad), hipMemcpyHostToDevice) != hipSuccess ||
+  uint16_t lut[LUT_N];
+  if (build_bucket_lut(hl.L, lut) > 2) return bail(-EIO);
+  if (hipMemcpy(c->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_lim_pad, lim_pad, sizeof(lim_pad), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
@@ -460,7 +505,7 @@ int l5dh_close(l5dh_ctx* c) {
     hipEventDestroy(e.b);
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
-  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
+  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
                   c->d_table, c->d_tile_tot, c->d_item_start, c->d_hot_list, c->d_header};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -468,7 +513,7 @@ int l5dh_close(l5dh_ctx* c) {
     if (s.tbase) hipFree(s.tbase);
     if (s.recs.p) hipFree(s.recs.p);
   }
-  DevBuf* bufs[] = {&c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
+  DevBuf* bufs[] = {&c->scratch1, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
                     &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
@@ -643,6 +688,10 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
         if (r) return r;
       }
       c->max_seg = (int)v;
+      return 0;
+    case L5DH_PARAM_BIN_MODE:
+      if (v < 0 || v > 2) return fail(c, -EINVAL, "bin mode must be 0 (auto), 1 (single) or 2 (two-level)");
+      c->bin_mode = (int)v;
       return 0;
     default:
       return fail(c, -EINVAL, "unknown parameter");

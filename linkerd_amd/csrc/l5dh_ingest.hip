@@ -1,0 +1,435 @@
+// l5dh_ingest.hip -- ingest-side kernels (Metric.Stat.add, batched).
+//
+//   k_count    LDS tile histogram of each slab of the COO batch -> table[g][t]
+//   k_colscan  per tile, exclusive prefix over slabs (in place) + tile totals
+//   k_tilescan exclusive prefix over tiles -> tile_base[F+1] (final layout)
+//   k_bin1     level 1: slab -> super-tiles (64 tiles), LDS counting sort of
+//              8K-sample sub-chunks, run writes; payload = truncated sample
+//   k_bin2     level 2: (super-tile, slab block) -> per-(slab, tile) segments,
+//              bucket by LUT-bracketed search, final 4-byte records
+//   k_bin      single-level alternative (bucketize + direct scatter)
+//
+// Final record (u32): [31:27] series in tile | [26:16] bucket | [15:0] off,
+//   off = contribution - base[bucket] when < 0xFFFF, else 0xFFFF and the exact
+//   difference went to sumfix[series] (integer atomics, order free).
+// Level-1 record: [31:26] tile in super-tile | [25:21] series in tile |
+//   [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped).
+#include "l5dh_device.hpp"
+
+namespace l5dh {
+namespace {
+
+constexpr int ST_TILES = 64;
+constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
+constexpr uint32_t V_ESC = (1u << 21) - 2048u;
+constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
+constexpr int CH1 = 8192;     // samples per level-1 sub-chunk (16 per thread)
+constexpr int FS_MAX = 512;
+constexpr int B2_NT = 256;
+constexpr int B2_GBLK = 8;    // slabs per k_bin2 item
+
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ series, size_t n, size_t per, uint32_t S,
+                                              uint32_t F, uint32_t* __restrict__ table, uint32_t* __restrict__ err,
+                                              int vec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* cnt = smem;
+  for (uint32_t t = threadIdx.x; t < F; t += WG) cnt[t] = 0;
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * per;
+  const size_t hi = lo + per < n ? lo + per : n;
+  bool bad = false;
+  auto one = [&](uint32_t s) {
+    if (s < S)
+      atomicAdd(&cnt[s >> TILE_SHIFT], 1u);
+    else
+      bad = true;
+  };
+  if (lo < hi) {
+    size_t done = lo;
+    if (vec) {  // lo and the base pointer are 16-B aligned
+      const size_t nv = (hi - lo) >> 2;
+      const uint4* __restrict__ p = reinterpret_cast<const uint4*>(series + lo);
+      size_t i = threadIdx.x;
+      for (; i + 3 * WG < nv; i += 4 * WG) {
+        const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
+        one(a.x); one(a.y); one(a.z); one(a.w);
+        one(b.x); one(b.y); one(b.z); one(b.w);
+        one(c.x); one(c.y); one(c.z); one(c.w);
+        one(d.x); one(d.y); one(d.z); one(d.w);
+      }
+      for (; i < nv; i += WG) {
+        const uint4 a = p[i];
+        one(a.x); one(a.y); one(a.z); one(a.w);
+      }
+      done = lo + (nv << 2);
+    }
+    for (size_t i = done + threadIdx.x; i < hi; i += WG) one(series[i]);
+  }
+  if (bad) atomicOr(err, 1u);
+  __syncthreads();
+  uint32_t* row = table + (size_t)blockIdx.x * F;
+  for (uint32_t t = threadIdx.x; t < F; t += WG) row[t] = cnt[t];
+}
+
+// WG = 64 tiles x 16 slab groups.
+__global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, int G, uint32_t F,
+                                                  uint32_t* __restrict__ tile_tot) {
+  __shared__ uint32_t part[16][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const uint32_t t = blockIdx.x * 64 + lane;
+  const int gper = (G + 15) / 16;
+  const int g0 = w * gper;
+  const int g1 = min(G, g0 + gper);
+  uint32_t s = 0;
+  if (t < F)
+    for (int g = g0; g < g1; ++g) s += table[(size_t)g * F + t];
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t v = part[k][lane];
+      part[k][lane] = acc;
+      acc += v;
+    }
+    if (t < F) tile_tot[t] = acc;
+  }
+  __syncthreads();
+  if (t < F) {
+    uint32_t acc = part[w][lane];
+    for (int g = g0; g < g1; ++g) {
+      const size_t i = (size_t)g * F + t;
+      const uint32_t v = table[i];
+      table[i] = acc;
+      acc += v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_tilescan(const uint32_t* __restrict__ tile_tot, uint32_t F,
+                                                   uint32_t* __restrict__ tile_base) {
+  __shared__ uint32_t lds[17];
+  const uint32_t per = (F + 1023) / 1024;
+  const uint32_t t0 = threadIdx.x * per;
+  uint32_t s = 0;
+  for (uint32_t k = 0; k < per; ++k)
+    if (t0 + k < F) s += tile_tot[t0 + k];
+  uint32_t tot;
+  uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
+  for (uint32_t k = 0; k < per; ++k)
+    if (t0 + k < F) {
+      tile_base[t0 + k] = acc;
+      acc += tile_tot[t0 + k];
+    }
+  if (threadIdx.x == 0) tile_base[F] = tot;
+}
+
+// Final record of one sample; escapes add their exact sum difference to sumfix.
+__device__ __forceinline__ uint32_t final_record(uint32_t s, float f, const uint16_t* __restrict__ lut,
+                                                 const int32_t* __restrict__ lim, int64_t* __restrict__ sumfix) {
+  int64_t c;
+  const uint32_t b = bucketize(f, lut, lim, c);
+  const int64_t off = c - (b ? (int64_t)lim[b - 1] : 0);
+  uint32_t o;
+  if ((uint64_t)off < (uint64_t)OFF_ESC) {
+    o = (uint32_t)off;
+  } else {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)off);
+    o = OFF_ESC;
+  }
+  return ((s & (TILE - 1)) << 27) | (b << 16) | o;
+}
+
+// Single-level: bucketize + scatter to the slab's exclusive (slab, tile) segment.
+__global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                            size_t n, size_t per, uint32_t S, uint32_t F,
+                                            const uint32_t* __restrict__ table, const uint32_t* __restrict__ tile_base,
+                                            Tables tb, uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
+                                            int vec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  int32_t* lim = reinterpret_cast<int32_t*>(smem);
+  uint16_t* lut = reinterpret_cast<uint16_t*>(smem + LIM_PAD);
+  uint32_t* cur = smem + LIM_PAD + LUT_N / 2;
+  for (int i = threadIdx.x; i < LIM_PAD; i += WG) lim[i] = tb.lim_pad[i];
+  for (int i = threadIdx.x; i < LUT_N; i += WG) lut[i] = tb.lut[i];
+  const uint32_t* row = table + (size_t)blockIdx.x * F;
+  for (uint32_t t = threadIdx.x; t < F; t += WG) cur[t] = tile_base[t] + row[t];
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * per;
+  const size_t hi = lo + per < n ? lo + per : n;
+  if (lo >= hi) return;
+  auto one = [&](uint32_t s, float f) {
+    if (s >= S) return;
+    const uint32_t rec = final_record(s, f, lut, lim, sumfix);
+    records[atomicAdd(&cur[s >> TILE_SHIFT], 1u)] = rec;
+  };
+  size_t done = lo;
+  if (vec) {
+    const size_t nv = (hi - lo) >> 2;
+    const uint4* ps = reinterpret_cast<const uint4*>(series + lo);
+    const float4* pv = reinterpret_cast<const float4*>(values + lo);
+    for (size_t i = threadIdx.x; i < nv; i += WG) {
+      const uint4 s = ps[i];
+      const float4 f = pv[i];
+      one(s.x, f.x); one(s.y, f.y); one(s.z, f.z); one(s.w, f.w);
+    }
+    done = lo + (nv << 2);
+  }
+  for (size_t i = done + threadIdx.x; i < hi; i += WG) one(series[i], values[i]);
+}
+
+// ------------------------------------------------------------------------
+// Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
+__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
+  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
+  int64_t c;
+  const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
+  if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
+  const int64_t off = c - (b ? (int64_t)tb.lim_pad[b - 1] : 0);
+  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)off);
+  return V_ESC + b;
+}
+
+__global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                                size_t n, size_t per, uint32_t S, uint32_t F,
+                                                const uint32_t* __restrict__ pre,
+                                                const uint32_t* __restrict__ tile_base, Tables tb,
+                                                uint32_t* __restrict__ out1, int64_t* __restrict__ sumfix, int vec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t lds9[B1_NT / 64 + 1];
+  uint32_t* stage = smem;                                         // [CH1]
+  uint16_t* stage_st = reinterpret_cast<uint16_t*>(smem + CH1);   // [CH1]
+  uint32_t* stcnt = smem + CH1 + CH1 / 2;                         // [FS_MAX]
+  uint32_t* stoff = stcnt + FS_MAX;
+  uint32_t* stcur = stoff + FS_MAX;
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t* prow = pre + (size_t)blockIdx.x * F;
+  for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
+    const uint32_t t0 = j * ST_TILES;
+    const uint32_t t1 = min(F, t0 + ST_TILES);
+    uint32_t acc = tile_base[t0];
+    for (uint32_t t = t0; t < t1; ++t) acc += prow[t];
+    stcur[j] = acc;
+    stcnt[j] = 0;
+  }
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * per;
+  const size_t hi = lo + per < n ? lo + per : n;
+  constexpr int PT = CH1 / B1_NT;  // 16 samples per thread: 4 groups of 4 consecutive
+  for (size_t c0 = lo; c0 < hi; c0 += CH1) {
+    uint32_t rec[PT], rank[PT];
+    uint32_t stv[PT];
+    uint32_t sv[PT];
+    float fv[PT];
+#pragma unroll
+    for (int k = 0; k < PT / 4; ++k) {
+      const size_t base = c0 + 4 * ((size_t)k * B1_NT + threadIdx.x);
+      if (vec && base + 3 < hi) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
+        const float4 f4 = *reinterpret_cast<const float4*>(values + base);
+        sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
+        fv[4 * k] = f4.x; fv[4 * k + 1] = f4.y; fv[4 * k + 2] = f4.z; fv[4 * k + 3] = f4.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = base + e < hi;
+          sv[4 * k + e] = in ? series[base + e] : 0xFFFFFFFFu;
+          fv[4 * k + e] = in ? values[base + e] : 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t s = sv[k];
+      stv[k] = 0xFFFFFFFFu;
+      if (s < S) {
+        const uint32_t pl = payload1(s, fv[k], tb, sumfix);
+        rec[k] = (((s >> TILE_SHIFT) & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl;
+        stv[k] = s >> ST_SHIFT;
+        rank[k] = atomicAdd(&stcnt[stv[k]], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t tot;
+    {
+      const uint32_t v = threadIdx.x < FS ? stcnt[threadIdx.x] : 0u;
+      const uint32_t e = block_excl_scan<B1_NT>(v, lds9, &tot);
+      if (threadIdx.x < FS) stoff[threadIdx.x] = e;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      if (stv[k] != 0xFFFFFFFFu) {
+        const uint32_t pos = stoff[stv[k]] + rank[k];
+        stage[pos] = rec[k];
+        stage_st[pos] = (uint16_t)stv[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += B1_NT) {
+      const uint32_t j = stage_st[i];
+      out1[stcur[j] + (i - stoff[j])] = stage[i];
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
+      stcur[j] += stcnt[j];
+      stcnt[j] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// Level 2.  Item = (super-tile j, block of B2_GBLK slabs).  The block's (j, g)
+// level-1 segments are contiguous, so the item streams one flat range; each
+// record goes to its per-(g, tile) final segment via an LDS cursor.
+__global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out1, uint32_t F, int G,
+                                                const uint32_t* __restrict__ pre,
+                                                const uint32_t* __restrict__ tile_tot,
+                                                const uint32_t* __restrict__ tile_base, Tables tb,
+                                                uint32_t* __restrict__ records) {
+  __shared__ int32_t lim[LIM_PAD];
+  __shared__ uint16_t lut[LUT_N];
+  __shared__ uint32_t cur[B2_GBLK][ST_TILES];
+  __shared__ uint32_t seg[B2_GBLK + 1];
+  for (int i = threadIdx.x; i < LIM_PAD; i += B2_NT) lim[i] = tb.lim_pad[i];
+  for (int i = threadIdx.x; i < LUT_N; i += B2_NT) lut[i] = tb.lut[i];
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t j = blockIdx.x % FS;
+  const int g0 = (int)(blockIdx.x / FS) * B2_GBLK;
+  const int ng = min(B2_GBLK, G - g0);
+  const uint32_t t0 = j * ST_TILES;
+  const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  // cursors of the block's slabs; segment lengths
+  for (int gi = w; gi < B2_GBLK; gi += B2_NT / 64) {
+    uint32_t p = 0, c = 0;
+    if (gi < ng && (uint32_t)lane < nt) {
+      const int g = g0 + gi;
+      const uint32_t t = t0 + lane;
+      p = pre[(size_t)g * F + t];
+      const uint32_t nxt = (g + 1 < G) ? pre[(size_t)(g + 1) * F + t] : tile_tot[t];
+      c = nxt - p;
+      cur[gi][lane] = tile_base[t] + p;
+    }
+    uint32_t sp = p, sc = c;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      sp += __shfl_xor(sp, d, 64);
+      sc += __shfl_xor(sc, d, 64);
+    }
+    if (lane == 0) {
+      if (gi == 0) seg[0] = tile_base[t0] + sp;
+      seg[gi + 1] = sc;  // length for now
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = seg[0];
+    for (int gi = 0; gi < B2_GBLK; ++gi) {
+      a += seg[gi + 1];
+      seg[gi + 1] = a;  // end of segment gi
+    }
+  }
+  __syncthreads();
+  const uint32_t A = seg[0];
+  const uint32_t B = seg[B2_GBLK];
+  int gi = 0;
+  auto one = [&](uint32_t idx, uint32_t r) {
+    while (idx >= seg[gi + 1]) ++gi;  // indices only grow per thread
+    const uint32_t tl = r >> 26;
+    const uint32_t loc = (r >> 21) & 31u;
+    const uint32_t pl = r & 0x1FFFFFu;
+    uint32_t b, off;
+    if (pl < V_ESC) {
+      b = bucket_lut(pl, lut, lim);
+      off = pl - (b ? (uint32_t)lim[b - 1] : 0u);  // bucket width < 2^16 below V_ESC
+    } else {
+      b = pl - V_ESC;
+      off = OFF_ESC;
+    }
+    records[atomicAdd(&cur[gi][tl], 1u)] = (loc << 27) | (b << 16) | off;
+  };
+  // flat range [A, B): head to 16-B alignment, then 2 x uint4 per thread per step
+  const uint32_t A4 = min(B, (A + 3u) & ~3u);
+  if (A + threadIdx.x < A4) one(A + threadIdx.x, out1[A + threadIdx.x]);
+  const uint32_t nv = (B - A4) >> 2;
+  const uint4* __restrict__ p = reinterpret_cast<const uint4*>(out1 + A4);
+  uint32_t i = threadIdx.x;
+  for (; i + B2_NT < nv; i += 2 * B2_NT) {
+    const uint4 x = p[i];
+    const uint4 y = p[i + B2_NT];
+    const uint32_t bx = A4 + 4 * i, by = A4 + 4 * (i + B2_NT);
+    one(bx, x.x); one(bx + 1, x.y); one(bx + 2, x.z); one(bx + 3, x.w);
+    one(by, y.x); one(by + 1, y.y); one(by + 2, y.z); one(by + 3, y.w);
+  }
+  if (i < nv) {
+    const uint4 x = p[i];
+    const uint32_t bx = A4 + 4 * i;
+    one(bx, x.x); one(bx + 1, x.y); one(bx + 2, x.z); one(bx + 3, x.w);
+  }
+  const uint32_t tt = A4 + (nv << 2) + threadIdx.x;
+  if (tt < B) {
+    gi = 0;
+    one(tt, out1[tt]);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------
+hipError_t set_ingest_attributes() {
+  hipError_t e;
+  const int big = 160 * 1024;
+  if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BIN1_LDS)))
+    return e;
+  return hipSuccess;
+}
+
+hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
+                        uint32_t* table, uint32_t* err, bool vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), (size_t)F * 4, st, series, n, per, S, F, table, err, vec ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* tile_tot, hipStream_t st) {
+  hipLaunchKernelGGL(k_colscan, dim3((F + 63) / 64), dim3(1024), 0, st, table, G, F, tile_tot);
+  return hipGetLastError();
+}
+
+hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_base, hipStream_t st) {
+  hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(1024), 0, st, tile_tot, F, tile_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
+                      uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
+                      int64_t* sumfix, bool vec, hipStream_t st) {
+  const size_t lds = (size_t)LIM_PAD * 4 + LUT_N * 2 + (size_t)F * 4;
+  hipLaunchKernelGGL(k_bin, dim3(G), dim3(WG), lds, st, series, values, n, per, S, F, table, tile_base, tb, records,
+                     sumfix, vec ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
+                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, uint32_t* scratch1,
+                       int64_t* sumfix, bool vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_bin1, dim3(G), dim3(B1_NT), BIN1_LDS, st, series, values, n, per, S, F, pre, tile_base, tb,
+                     scratch1, sumfix, vec ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin2(const uint32_t* scratch1, int G, uint32_t F, const uint32_t* pre, const uint32_t* tile_tot,
+                       const uint32_t* tile_base, Tables tb, uint32_t* records, hipStream_t st) {
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const int nb = (G + B2_GBLK - 1) / B2_GBLK;
+  hipLaunchKernelGGL(k_bin2, dim3(FS * nb), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_tot, tile_base, tb,
+                     records);
+  return hipGetLastError();
+}
+
+}  // namespace l5dh

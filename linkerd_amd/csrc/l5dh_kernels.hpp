@@ -26,10 +26,13 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 // LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows (hot)
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + 16 * 8 + 64;
 
-struct Tables {            // constant tables in HBM (7-8 KB each, L2 resident)
-  const int32_t* lim_pad;  // [2048]
+constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
+
+struct Tables {            // constant tables in HBM (a few KB each, L2 resident)
+  const int32_t* lim_pad;  // [2048] limits padded with Int.MaxValue
   const int32_t* mid;      // [1798] value reported for bucket b
-  const int32_t* base;     // [1798] lower limit of bucket b (0 for b == 0)
+  const int32_t* base;     // [1800] lower limit of bucket b (0 for b == 0), zero padded
+  const uint16_t* lut;     // [LUT_N] lower bound of the bucket of each LUT interval
 };
 
 struct Segs {              // binned ingest batches awaiting aggregation
@@ -73,6 +76,14 @@ hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
                       int64_t* sumfix, bool vec, hipStream_t st);
+// Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
+// (super-tile -> tiles).  scratch1 holds n level-1 records.
+constexpr size_t BIN1_LDS = (size_t)8192 * 4 + 8192 * 2 + 3 * 512 * 4;
+hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
+                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, uint32_t* scratch1,
+                       int64_t* sumfix, bool vec, hipStream_t st);
+hipError_t launch_bin2(const uint32_t* scratch1, int G, uint32_t F, const uint32_t* pre, const uint32_t* tile_tot,
+                       const uint32_t* tile_base, Tables tb, uint32_t* records, hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
                        hipStream_t st);
 hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st);
@@ -84,6 +95,10 @@ hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb
 // dense rows ext[count][1798] + ext_total[count].
 hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out,
                        int reset, int64_t* totals_out, hipStream_t st);
-hipError_t set_kernel_attributes();
+hipError_t set_ingest_attributes();
+hipError_t set_snapshot_attributes();
+// LUT for bucket_lut: builds lut[LUT_N] from the limits; returns the largest
+// number of limits inside one LUT interval (the device search assumes <= 2).
+int build_bucket_lut(const int32_t* limits, uint16_t* lut);
 
 }  // namespace l5dh

@@ -1,0 +1,356 @@
+// l5dh_snapshot.hip -- snapshot-side kernels (Metric.Stat.snapshot/reset/summary,
+// batched as AdminMetricsExportTelemeter.snapshotHistograms drives them).
+//
+//   k_plan       per tile: records over pending segments, cold/hot, work items
+//   k_hot_init   zero the state rows of clean hot tiles
+//   k_accum      cold tile: 32 series in u16-packed LDS bins, fused summary +
+//                dense flush; hot tile: (half, chunk) partial in u32 LDS bins,
+//                flushed with global atomics
+//   k_hot_finish summaries of hot tiles from their merged state rows
+//   k_rows       summaries / dense copies of state rows or external rows
+#include "l5dh_device.hpp"
+
+namespace l5dh {
+namespace {
+
+// k_plan: one workgroup.  Per tile: records across segments, hot/cold, work
+// items; exclusive scans -> item_start[F+1], hot_list, header {items, hot}.
+__global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
+                                               uint32_t hot_chunk, Plan plan) {
+  __shared__ uint32_t lds_a[17];
+  __shared__ uint32_t lds_b[17];
+  const uint32_t per = (F + 1023) / 1024;
+  const uint32_t t0 = threadIdx.x * per;
+  uint32_t items = 0, hot = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t t = t0 + k;
+    if (t >= F) break;
+    uint32_t tot = 0;
+    for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
+    plan.tile_tot[t] = tot;
+    if (tot > cold_limit) {
+      items += 2u * ((tot + hot_chunk - 1) / hot_chunk);
+      hot += 1;
+    } else if (final_mode || tot > 0) {
+      items += 1;
+    }
+  }
+  uint32_t tot_items, tot_hot;
+  uint32_t ia = block_excl_scan<1024>(items, lds_a, &tot_items);
+  uint32_t ha = block_excl_scan<1024>(hot, lds_b, &tot_hot);
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t t = t0 + k;
+    if (t >= F) break;
+    const uint32_t tot = plan.tile_tot[t];
+    plan.item_start[t] = ia;
+    if (tot > cold_limit) {
+      ia += 2u * ((tot + hot_chunk - 1) / hot_chunk);
+      plan.hot_list[ha++] = t;
+    } else if (final_mode || tot > 0) {
+      ia += 1;
+    }
+  }
+  if (threadIdx.x == 0) {
+    plan.item_start[F] = tot_items;
+    plan.header[0] = tot_items;
+    plan.header[1] = tot_hot;
+  }
+}
+
+// k_hot_init: split tiles accumulate with global atomics into state rows, so
+// clean ones start from zero.
+__global__ __launch_bounds__(256) void k_hot_init(const uint32_t* __restrict__ hot_list, State st) {
+  const uint32_t t = hot_list[blockIdx.x];
+  if (st.dirty[t]) return;
+  const uint32_t s0 = t * TILE;
+  const uint32_t s1 = min(st.S, s0 + TILE);
+  uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
+  const size_t n4 = (size_t)(s1 - s0) * ROW / 4;
+  for (size_t i = threadIdx.x; i < n4; i += 256) p[i] = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
+}
+
+__device__ __forceinline__ uint32_t find_tile(const uint32_t* __restrict__ item_start, uint32_t F, uint32_t item) {
+  // last t with item_start[t] <= item
+  uint32_t lo = 0, hi = F;  // invariant: item_start[lo] <= item < item_start[hi] (item_start[F] = total)
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (item_start[m] <= item) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+// k_accum: one work item = one tile (cold: <= cold_limit records, 32 series in
+// u16-packed LDS bins, fused summary + dense flush) or one (tile, half, chunk)
+// of a hot tile (16 series in u32 LDS bins, flushed with global atomics).
+__global__ __launch_bounds__(WG) void k_accum(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                              uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t item = blockIdx.x;
+  const uint32_t F = st.F;
+  const uint32_t t = find_tile(plan.item_start, F, item);
+  const uint32_t sub = item - plan.item_start[t];
+  const uint32_t tot = plan.tile_tot[t];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+
+  if (tot <= cold_limit) {
+    // ---------------- cold tile: single pass ----------------
+    uint32_t* hist = smem;                    // [32][900] u16 pairs
+    uint32_t* offsum = smem + TILE * CROW;    // [32]
+    {
+      uint4* p = reinterpret_cast<uint4*>(smem);
+      for (int i = threadIdx.x; i < TILE * CROW / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
+      if (threadIdx.x < TILE) offsum[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (int j = 0; j < segs.n; ++j) {
+      for_records<WG>(segs.recs[j], segs.tbase[j][t], segs.tbase[j][t + 1], [&](uint32_t rec) {
+        const uint32_t loc = rec >> 27;
+        const uint32_t b = (rec >> 16) & 0x7FFu;
+        const uint32_t off = rec & 0xFFFFu;
+        atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+        if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[loc], off);
+      });
+    }
+    __syncthreads();
+    const bool dirty = st.dirty[t] != 0;
+    const bool keep = !(final_mode && reset);
+    const int ng = lane_groups(lane);
+    for (int rep = 0; rep < 2; ++rep) {
+      const uint32_t loc = w + 16 * rep;
+      const uint32_t s = t * TILE + loc;
+      if (s >= st.S) continue;
+      const uint32_t oi = s - out.first;
+      const bool emit = final_mode && s >= out.first && oi < out.count;
+      int32_t* orow = (emit && out.counts) ? out.counts + (size_t)oi * NB : nullptr;
+      uint32_t* srow = st.counts + (size_t)s * ROW;
+      const SrcLds16 lds{hist + loc * CROW};
+      uint32_t g[9];
+      uint64_t bs = 0;  // sum_b newcount_b * base_b (+ sum(off) below) = exact sum of new samples
+      if (!dirty) {
+        // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are LDS padding)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = lane + 64 * k;
+          if (q < NB4) {
+            const int b0 = 4 * q;
+            const uint4 v = lds.get4(b0);
+            bs += dot4(v, tb.base, b0);
+            if (orow) store4_1798(orow, b0, v);
+            if (keep) store4_state(srow, b0, v);
+          }
+        }
+        // blocked group sums for the summary scan
+#pragma unroll
+        for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
+      } else {
+        const SrcRow32 old{srow};
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          g[q] = 0;
+          if (q < ng) {
+            const int b0 = 28 * lane + 4 * q;
+            const uint4 v = lds.get4(b0);
+            bs += dot4(v, tb.base, b0);
+            const uint4 o = old.get4(b0);
+            const uint4 cmb = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+            g[q] = sum4(cmb);
+            if (orow) store4_1798(orow, b0, cmb);
+            store4_state(srow, b0, cmb);  // the merged row is also the summary source
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      }
+      bs = wave_sum(bs);
+      int64_t total = (int64_t)bs + (int64_t)offsum[loc] + st.sumfix[s];
+      if (dirty) total += st.total[s];
+      if (lane == 0) {
+        st.sumfix[s] = 0;
+        if (keep) st.total[s] = total;
+      }
+      if (emit) {
+        Summary88* so = out.summ ? out.summ + oi : nullptr;
+        if (dirty)
+          wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
+        else
+          wave_summary(g, lds, total, tb.mid, so);
+      }
+    }
+    if (threadIdx.x == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
+  } else {
+    // ---------------- hot tile: split over (half, chunk) ----------------
+    uint32_t* hist = smem;                                                   // [16][1800] u32
+    unsigned long long* offsum = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16]
+    const uint32_t half = sub & 1u;
+    const uint32_t chunk = sub >> 1;
+    {
+      uint4* p = reinterpret_cast<uint4*>(smem);
+      for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
+      if (threadIdx.x < 16) offsum[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint64_t vlo = (uint64_t)chunk * hot_chunk;
+    const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
+    uint64_t vbase = 0;
+    for (int j = 0; j < segs.n; ++j) {
+      const uint32_t a = segs.tbase[j][t];
+      const uint32_t e = segs.tbase[j][t + 1];
+      const uint64_t len = e - a;
+      const uint64_t lo = vlo > vbase ? vlo : vbase;
+      const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+      if (lo < hi) {
+        const uint32_t ra = a + (uint32_t)(lo - vbase);
+        for_records<WG>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), [&](uint32_t rec) {
+          const uint32_t loc = rec >> 27;
+          if ((loc >> 4) != half) return;
+          const uint32_t l = loc & 15u;
+          const uint32_t b = (rec >> 16) & 0x7FFu;
+          const uint32_t off = rec & 0xFFFFu;
+          atomicAdd(&hist[l * HROW + b], 1u);
+          if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
+        });
+      }
+      vbase += len;
+    }
+    __syncthreads();
+    const uint32_t s = t * TILE + 16 * half + w;
+    if (s < st.S) {
+      uint32_t* grow = st.counts + (size_t)s * ROW;
+      const uint32_t* hrow = hist + w * HROW;
+      uint64_t bs = 0;
+      for (int b = lane; b < NB; b += 64) {
+        const uint32_t v = hrow[b];
+        if (v) {
+          bs += (uint64_t)v * (uint64_t)(uint32_t)tb.base[b];
+          atomicAdd(&grow[b], v);
+        }
+      }
+      bs = wave_sum(bs);
+      if (lane == 0) {
+        const uint64_t add = bs + offsum[w];
+        if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
+      }
+    }
+  }
+}
+
+// k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
+// write outputs, update state/dirty.
+__global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
+                                                   int reset) {
+  const uint32_t t = plan.hot_list[blockIdx.x >> 1];
+  const uint32_t half = blockIdx.x & 1u;
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const uint32_t s = t * TILE + 16 * half + w;
+  if (s < st.S) {
+    int64_t total = st.total[s] + st.sumfix[s];
+    if (final_mode) {
+      const uint32_t oi = s - out.first;
+      if (s >= out.first && oi < out.count) {
+        const SrcRow32 src{st.counts + (size_t)s * ROW};
+        uint32_t g[9];
+        row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
+        wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+      }
+    }
+    if (lane == 0) {
+      st.sumfix[s] = 0;
+      st.total[s] = total;
+    }
+  }
+  if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
+}
+
+// k_rows: one wave per series: summary / dense copy of state rows (range
+// snapshot, export) or of external dense rows (fleet merge).
+__global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restrict__ ext,
+                                              const int64_t* __restrict__ ext_total, Tables tb, Outputs out, int reset,
+                                              int64_t* __restrict__ totals_out) {
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= out.count) return;
+  const int lane = lane_id();
+  uint32_t g[9];
+  int32_t* orow = out.counts ? out.counts + (size_t)i * NB : nullptr;
+  if (ext) {
+    const SrcExt src{ext + (size_t)i * NB};
+    const int64_t total = ext_total ? ext_total[i] : 0;
+    row_pass(src, g, orow);
+    if (out.summ) wave_summary(g, src, total, tb.mid, out.summ + i);
+    if (totals_out && lane == 0) totals_out[i] = total;
+    return;
+  }
+  const uint32_t s = out.first + i;
+  const bool dirty = st.dirty[s >> TILE_SHIFT] != 0;
+  if (dirty) {
+    const SrcRow32 src{st.counts + (size_t)s * ROW};
+    const int64_t total = st.total[s];
+    row_pass(src, g, orow);
+    if (out.summ) wave_summary(g, src, total, tb.mid, out.summ + i);
+    if (totals_out && lane == 0) totals_out[i] = total;
+    if (reset) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      uint32_t* row = st.counts + (size_t)s * ROW;
+      const int ng = lane_groups(lane);
+#pragma unroll
+      for (int q = 0; q < 9; ++q)
+        if (q < ng) store4_state(row, 28 * lane + 4 * q, make_uint4(0u, 0u, 0u, 0u));
+      if (lane == 0) st.total[s] = 0;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) g[q] = 0;
+    if (orow) {
+      const int ng = lane_groups(lane);
+#pragma unroll
+      for (int q = 0; q < 9; ++q)
+        if (q < ng) store4_1798(orow, 28 * lane + 4 * q, make_uint4(0u, 0u, 0u, 0u));
+    }
+    if (out.summ) wave_summary(g, SrcRow32{st.counts}, 0, tb.mid, out.summ + i);  // num == 0: no bin is read
+    if (totals_out && lane == 0) totals_out[i] = 0;
+  }
+}
+
+}  // namespace
+
+hipError_t set_snapshot_attributes() {
+  return hipFuncSetAttribute((const void*)k_accum, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
+  return hipGetLastError();
+}
+
+hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st) {
+  if (num_hot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hot_init, dim3(num_hot), dim3(256), 0, st, plan.hot_list, state);
+  return hipGetLastError();
+}
+
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t num_items, State state, Tables tb, Outputs out,
+                        uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset, hipStream_t st) {
+  if (num_items == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_accum, dim3(num_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
+                     hot_chunk, final_mode, reset);
+  return hipGetLastError();
+}
+
+hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
+                             int reset, hipStream_t st) {
+  if (num_hot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hot_finish, dim3(num_hot * 2), dim3(WG), 0, st, plan, state, tb, out, final_mode, reset);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out, int reset,
+                       int64_t* totals_out, hipStream_t st) {
+  if (out.count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows, dim3((out.count + 3) / 4), dim3(256), 0, st, state, ext, ext_total, tb, out, reset,
+                     totals_out);
+  return hipGetLastError();
+}
+
+}  // namespace l5dh

@@ -1,0 +1,42 @@
+"""Extract the P5 pin from the reference's own admin-dashboard
+fixture: every histogram summary recorded in tree-mode /admin/metrics.json
+output (admin/src/main/resources/io/buoyant/admin/js/spec/fixtures/metrics.js).
+
+The fixture holds only summaries (raw samples are unknown), so it pins the
+summary *invariants*: min/max/percentiles are bucket midpoints, avg == sum/count
+as a Java double, count/sum consistency.  Run here (the reference is not on the
+GPU box); output: tests/golden/p5_fixture_summaries.json (data only).
+"""
+import json
+import os
+import re
+import sys
+
+SRC = "/root/reference/admin/src/main/resources/io/buoyant/admin/js/spec/fixtures/metrics.js"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "p5_fixture_summaries.json")
+
+
+def main(src=SRC, out=OUT):
+    text = open(src).read()
+    body = text[text.index("return") + len("return"):]
+    body = body[:body.rindex("}")]  # drop trailing ");" of define(...)
+    tree = json.loads(body[: body.rindex("}") + 1])
+    rows = []
+
+    def walk(node, path):
+        if isinstance(node, dict):
+            if "stat.count" in node:
+                rows.append({"path": "/".join(path), **{k[5:]: node[k] for k in node if k.startswith("stat.")}})
+            for k, v in node.items():
+                if isinstance(v, dict):
+                    walk(v, path + [k])
+
+    walk(tree, [])
+    with open(out, "w") as f:
+        json.dump({"source": "admin/src/main/resources/io/buoyant/admin/js/spec/fixtures/metrics.js",
+                   "summaries": rows}, f, indent=1, sort_keys=True)
+    print(f"wrote {len(rows)} summaries to {out}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

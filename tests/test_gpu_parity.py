@@ -20,9 +20,14 @@ EDGE_VALUES = np.array([
 ], dtype=np.float32)
 
 
-def _engine(S):
+def _engine(S, bin_mode=0):
     from linkerd_amd.engine import HistogramEngine
-    return HistogramEngine(S)
+    e = HistogramEngine(S)
+    e.set_param(N.PARAM_BIN_MODE, bin_mode)
+    return e
+
+
+BIN_MODES = pytest.mark.parametrize("bin_mode", [1, 2], ids=["single", "twolevel"])
 
 
 def _assert_summaries_equal(got, want, label=""):
@@ -53,11 +58,12 @@ def test_limits_match_oracle(oracle):
     np.testing.assert_array_equal(N.limits(), oracle.limits())
 
 
-def test_small_random_bitexact(oracle):
+@BIN_MODES
+def test_small_random_bitexact(oracle, bin_mode):
     rng = np.random.default_rng(11)
     S, n = 1000, 300_000
     series, vals = _random_batch(rng, S, n)
-    eng = _engine(S)
+    eng = _engine(S, bin_mode)
     eng.ingest(series, vals)
     got, counts = eng.snapshot(reset=True, with_counts=True)
     o = oracle.OracleHistograms(S)
@@ -70,14 +76,15 @@ def test_small_random_bitexact(oracle):
     assert (got2["count"] == 0).all() and (got2["sum"] == 0).all() and (got2["avg"] == 0).all()
 
 
-def test_edge_values_every_series(oracle):
+@BIN_MODES
+def test_edge_values_every_series(oracle, bin_mode):
     S = 70  # not a multiple of the 32-series tile
     series = np.repeat(np.arange(S, dtype=np.uint32), EDGE_VALUES.size)
     vals = np.tile(EDGE_VALUES, S)
     rng = np.random.default_rng(3)
     perm = rng.permutation(series.size)
     series, vals = series[perm], vals[perm]
-    eng = _engine(S)
+    eng = _engine(S, bin_mode)
     eng.ingest(series, vals)
     got, counts = eng.snapshot(with_counts=True)
     o = oracle.OracleHistograms(S)
@@ -105,11 +112,12 @@ def test_multi_batch_and_cumulative_snapshots(oracle, reset):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"iter {it}")
 
 
-def test_hot_tile_split_path(oracle):
+@BIN_MODES
+def test_hot_tile_split_path(oracle, bin_mode):
     """Force the split (hot-tile) path: small cold limit and chunk."""
     rng = np.random.default_rng(9)
     S = 100
-    eng = _engine(S)
+    eng = _engine(S, bin_mode)
     eng.set_param(N.PARAM_COLD_LIMIT, 500)
     eng.set_param(N.PARAM_HOT_CHUNK, 1024)
     o = oracle.OracleHistograms(S)
@@ -180,10 +188,11 @@ def test_invalid_series_reported(oracle):
     _assert_summaries_equal(got, o.snapshot(), "invalid dropped")
 
 
-def test_c2_slice_bitexact(oracle):
+@BIN_MODES
+def test_c2_slice_bitexact(oracle, bin_mode):
     """C2 recipe at 1/10 of the series: 10k series x 1k samples."""
     series, vals = synth.c2(S=10_000, K=1_000)
-    eng = _engine(10_000)
+    eng = _engine(10_000, bin_mode)
     eng.ingest(series, vals)
     got, counts = eng.snapshot(with_counts=True)
     o = oracle.OracleHistograms(10_000)
@@ -210,3 +219,34 @@ def test_device_buffers_in_and_out(oracle):
     o.ingest(series, vals)
     np.testing.assert_array_equal(cnt.cpu().numpy(), o.counts())
     _assert_summaries_equal(got, o.snapshot(), "device io")
+
+
+@pytest.mark.parametrize("name", ["mixed64", "c1_100k", "c2_200x500", "c3_zipf1000"])
+def test_golden_vectors(name):
+    """Committed golden fixtures (tests/golden/make_golden.py) reproduced on the GPU."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"golden_{name}.npz"))
+    S = int(g["nseries"])
+    eng = _engine(S)
+    eng.ingest(g["series"], g["values"])
+    got, counts = eng.snapshot(with_counts=True)
+    np.testing.assert_array_equal(counts, g["counts"])
+    assert got.view(np.uint8).reshape(S, 88).tobytes() == g["summaries"].tobytes()
+
+
+@BIN_MODES
+def test_zipf_series_space_1m(oracle, bin_mode):
+    """1M-series engine (F = 32768 tiles, 512 super-tiles) on a Zipf C3 slice."""
+    S = 1_000_000
+    series, vals = synth.c3(S=S, N=2_000_000)
+    eng = _engine(S, bin_mode)
+    eng.ingest(series, vals)
+    got, counts = eng.snapshot(with_counts=True)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals, threads=8)
+    want_counts = o.counts()
+    want = o.snapshot()
+    _assert_summaries_equal(got, want, "zipf 1M")
+    touched = np.unique(series)
+    np.testing.assert_array_equal(counts[touched], want_counts[touched])
+    assert counts.sum() == series.size

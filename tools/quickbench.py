@@ -8,8 +8,12 @@ from linkerd_amd.engine import HistogramEngine
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000
+MODE = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 t0 = time.time()
-series, vals = synth.c2(S=S, K=K)
+if len(sys.argv) > 4 and sys.argv[4] == "zipf":
+    series, vals = synth.c3(S=S, N=S * K)
+else:
+    series, vals = synth.c2(S=S, K=K)
 print(f"gen {time.time()-t0:.1f}s", flush=True)
 ds = torch.from_numpy(series.view(np.int32)).cuda()
 dv = torch.from_numpy(vals).cuda()
@@ -17,7 +21,9 @@ eng = HistogramEngine(S)
 summ = torch.zeros(S * 11, dtype=torch.int64, device="cuda")
 cnt = torch.zeros((S, 1798), dtype=torch.int32, device="cuda")
 eng.set_param(N.PARAM_TIMING, 1)
-for it in range(8):
+eng.set_param(N.PARAM_BIN_MODE, MODE)
+print("mode", MODE)
+for it in range(5):
     torch.cuda.synchronize()
     t = time.perf_counter()
     eng.ingest(ds, dv)
