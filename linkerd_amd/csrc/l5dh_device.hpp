@@ -281,6 +281,64 @@ __device__ __forceinline__ uint32_t bucketize(float f, const uint16_t* __restric
   return (key >= 0 && key < INT_MAXV) ? bucket_lut((uint32_t)key, lut, lim) : search_key(key, lim);
 }
 
+// Number of set bits of m below this lane.
+__device__ __forceinline__ uint32_t mask_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave-aggregated LDS counters for skewed keys (Zipf heads).  Same result as
+// every valid lane doing `atomicAdd(&ctr[key], 1)` (the returned ranks are a
+// permutation of what that would return), but up to ROUNDS leader rounds merge
+// the lanes that share the leading lane's key into one atomic; aggregation stops
+// as soon as a leader's key is unique in the wave.  Must be called by the whole
+// wave (convergent).
+template <int ROUNDS>
+__device__ __forceinline__ uint32_t wave_atomic_rank(uint32_t* ctr, uint32_t key, bool valid) {
+  unsigned long long active = __ballot(valid);
+  uint32_t rank = 0;
+  bool done = !valid;
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    if (!active) break;
+    const int leader = __ffsll((long long)active) - 1;
+    const uint32_t lk = __shfl(key, leader, 64);
+    const bool mine = !done && key == lk;
+    const unsigned long long m = __ballot(mine);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(&ctr[lk], cnt);
+    base = __shfl(base, leader, 64);
+    if (mine) {
+      rank = base + mask_below(m);
+      done = true;
+    }
+    active &= ~m;
+    if (cnt == 1) break;
+  }
+  if (!done) rank = atomicAdd(&ctr[key], 1u);
+  return rank;
+}
+
+template <int ROUNDS>
+__device__ __forceinline__ void wave_atomic_inc(uint32_t* ctr, uint32_t key, bool valid) {
+  unsigned long long active = __ballot(valid);
+  bool done = !valid;
+#pragma unroll
+  for (int r = 0; r < ROUNDS; ++r) {
+    if (!active) break;
+    const int leader = __ffsll((long long)active) - 1;
+    const uint32_t lk = __shfl(key, leader, 64);
+    const bool mine = !done && key == lk;
+    const unsigned long long m = __ballot(mine);
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    if (lane_id() == leader) atomicAdd(&ctr[lk], cnt);
+    if (mine) done = true;
+    active &= ~m;
+    if (cnt == 1) break;
+  }
+  if (!done) atomicAdd(&ctr[key], 1u);
+}
+
 // Visit records r[a, e) with 16-B loads, two in flight per thread per step.
 template <int NT, class Fn>
 __device__ __forceinline__ void for_records(const uint32_t* __restrict__ r, uint32_t a, uint32_t e, Fn&& fn) {

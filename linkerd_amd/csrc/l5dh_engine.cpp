@@ -116,8 +116,10 @@ struct l5dh_ctx {
   uint32_t* d_table = nullptr;  // [G_max][F]
   uint32_t* d_tile_tot = nullptr;
   uint32_t* d_item_start = nullptr;
+  uint32_t* d_item_start2 = nullptr;
   uint32_t* d_hot_list = nullptr;
   uint32_t* d_header = nullptr;
+  uint32_t* d_b2plan = nullptr;  // level-2 item plan [2*FS+2]
   uint32_t* h_header = nullptr;  // pinned
   int G_max = 256;
   // segments
@@ -135,7 +137,7 @@ struct l5dh_ctx {
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
-  uint32_t hot_chunk = 1u << 20;
+  uint32_t hot_chunk = 1u << 18;  // records per hot item: the second half-round re-reads them from L2
   bool timing = false;
   struct Ev {
     int kid;
@@ -248,7 +250,9 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
-Plan plan(l5dh_ctx* c) { return Plan{c->d_tile_tot, c->d_item_start, c->d_hot_list, c->d_header}; }
+Plan plan(l5dh_ctx* c) {
+  return Plan{c->d_tile_tot, c->d_item_start, c->d_item_start2, c->d_hot_list, c->d_header};
+}
 
 Segs segs_view(l5dh_ctx* c) {
   Segs s{};
@@ -270,10 +274,11 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, pl, c->stream));
   }
-  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 12, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const uint32_t items = c->h_header[0];
+  const uint32_t cold_items = c->h_header[0];
   const uint32_t hot = c->h_header[1];
+  const uint32_t hot_items = c->h_header[2];
   State st = state(c);
   Tables tb = tables(c);
   if (hot) {
@@ -282,7 +287,8 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   }
   {
     KTimer kt(c, L5DH_K_ACCUM);
-    HIPCHK(c, launch_accum(sv, pl, items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset, c->stream));
+    HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
+                           c->stream));
   }
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
@@ -350,7 +356,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   const bool two_level = c->bin_mode != 1;
   if (two_level) {
-    int r = ensure(c, c->scratch1, n * 4);
+    int r = ensure(c, c->scratch1, n * 4 + 16);  // k_bin2 reads whole 16-B groups
     if (r) return r;
     {
       KTimer kt(c, L5DH_K_BIN);
@@ -358,8 +364,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
                             static_cast<uint32_t*>(c->scratch1.p), c->d_sumfix, vec, c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
-    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), G, c->F, c->d_table, c->d_tile_tot, sg.tbase,
-                          tables(c), static_cast<uint32_t*>(sg.recs.p), c->stream));
+    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, c->d_tile_tot, sg.tbase,
+                          tables(c), c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->stream));
   } else {
     KTimer kt(c, L5DH_K_BIN);
     HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
@@ -468,8 +474,9 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 2) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
-            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) &&
-            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16);
+            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
+            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
+            mal((void**)&c->d_b2plan, 4 * 1026);
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
   if (!ok) {
     (void)hipGetLastError();
@@ -506,7 +513,7 @@ int l5dh_close(l5dh_ctx* c) {
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
-                  c->d_table, c->d_tile_tot, c->d_item_start, c->d_hot_list, c->d_header};
+                  c->d_table, c->d_tile_tot, c->d_item_start, c->d_item_start2, c->d_hot_list, c->d_header, c->d_b2plan};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
@@ -677,7 +684,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->cold_limit = (uint32_t)v;
       return 0;
     case L5DH_PARAM_HOT_CHUNK:
-      if (v < 1024 || v > (1ll << 30)) return fail(c, -EINVAL, "hot chunk must be in [1024, 2^30]");
+      if (v < 65536 || v > (1ll << 30)) return fail(c, -EINVAL, "hot chunk must be in [65536, 2^30]");
       c->hot_chunk = (uint32_t)v;
       return 0;
     case L5DH_PARAM_MAX_SEGMENTS:

@@ -26,7 +26,8 @@ constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
 constexpr int CH1 = 8192;     // samples per level-1 sub-chunk (16 per thread)
 constexpr int FS_MAX = 512;
 constexpr int B2_NT = 256;
-constexpr int B2_GBLK = 8;    // slabs per k_bin2 item
+constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
+constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
 
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ series, size_t n, size_t per, uint32_t S,
@@ -40,10 +41,9 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
   const size_t hi = lo + per < n ? lo + per : n;
   bool bad = false;
   auto one = [&](uint32_t s) {
-    if (s < S)
-      atomicAdd(&cnt[s >> TILE_SHIFT], 1u);
-    else
-      bad = true;
+    const bool ok = s < S;
+    bad |= !ok;
+    wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
   };
   if (lo < hi) {
     size_t done = lo;
@@ -51,20 +51,34 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const size_t nv = (hi - lo) >> 2;
       const uint4* __restrict__ p = reinterpret_cast<const uint4*>(series + lo);
       size_t i = threadIdx.x;
-      for (; i + 3 * WG < nv; i += 4 * WG) {
+      const size_t wlast = threadIdx.x | 63;  // last lane of this wave: uniform loop bound
+      for (; wlast - threadIdx.x + i + 3 * WG < nv; i += 4 * WG) {
         const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
         one(a.x); one(a.y); one(a.z); one(a.w);
         one(b.x); one(b.y); one(b.z); one(b.w);
         one(c.x); one(c.y); one(c.z); one(c.w);
         one(d.x); one(d.y); one(d.z); one(d.w);
       }
-      for (; i < nv; i += WG) {
-        const uint4 a = p[i];
-        one(a.x); one(a.y); one(a.z); one(a.w);
+      for (; i - threadIdx.x < nv; i += WG) {  // convergent: out-of-range lanes pass invalid ids
+        uint4 a = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (i < nv) a = p[i];
+        const bool in = i < nv;
+        auto one_in = [&](uint32_t s) {
+          const bool ok = in && s < S;
+          bad |= in && !ok;
+          wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
+        };
+        one_in(a.x); one_in(a.y); one_in(a.z); one_in(a.w);
       }
       done = lo + (nv << 2);
     }
-    for (size_t i = done + threadIdx.x; i < hi; i += WG) one(series[i]);
+    for (size_t i0 = done; i0 < hi; i0 += WG) {  // convergent tail (the aggregation needs whole waves)
+      const size_t i = i0 + threadIdx.x;
+      const uint32_t s = i < hi ? series[i] : 0xFFFFFFFFu;
+      const bool ok = s < S;
+      bad |= i < hi && !ok;
+      wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
+    }
   }
   if (bad) atomicOr(err, 1u);
   __syncthreads();
@@ -244,12 +258,13 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
     for (int k = 0; k < PT; ++k) {
       const uint32_t s = sv[k];
       stv[k] = 0xFFFFFFFFu;
-      if (s < S) {
+      const bool ok = s < S;
+      if (ok) {
         const uint32_t pl = payload1(s, fv[k], tb, sumfix);
         rec[k] = (((s >> TILE_SHIFT) & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl;
         stv[k] = s >> ST_SHIFT;
-        rank[k] = atomicAdd(&stcnt[stv[k]], 1u);
       }
+      rank[k] = wave_atomic_rank<3>(stcnt, ok ? stv[k] : 0u, ok);
     }
     __syncthreads();
     uint32_t tot;
@@ -281,99 +296,154 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   }
 }
 
-// Level 2.  Item = (super-tile j, block of B2_GBLK slabs).  The block's (j, g)
-// level-1 segments are contiguous, so the item streams one flat range; each
-// record goes to its per-(g, tile) final segment via an LDS cursor.
+// Level-2 plan (one workgroup): per super-tile j, nb_j items of equal slab
+// ranges so that every item holds about B2_ITEM records (skew-balanced).
+// plan[0..FS] = item_start, plan[FS+1 .. 2FS] = slab range size per ST.
+__global__ __launch_bounds__(1024) void k_bin2plan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
+                                                   uint32_t* __restrict__ plan) {
+  __shared__ uint32_t lds[17];
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  uint32_t nb = 0, gsz = 0;
+  const uint32_t j = threadIdx.x;
+  if (j < FS) {
+    uint64_t tot = 0;
+    const uint32_t t1 = min(F, (j + 1) * ST_TILES);
+    for (uint32_t t = j * ST_TILES; t < t1; ++t) tot += tile_tot[t];
+    uint32_t want = (uint32_t)((tot + B2_ITEM - 1) / B2_ITEM);
+    want = max(1u, min(want, (uint32_t)G));
+    gsz = ((uint32_t)G + want - 1) / want;
+    nb = ((uint32_t)G + gsz - 1) / gsz;
+  }
+  uint32_t total;
+  const uint32_t e = block_excl_scan<1024>(nb, lds, &total);
+  if (j < FS) {
+    plan[j] = e;
+    plan[FS + 1 + j] = gsz;
+  }
+  if (threadIdx.x == 0) plan[FS] = total;
+}
+
+// Level 2.  Item = (super-tile j, slab range [g0, g1)).  Its level-1 records are
+// one contiguous range; tile t's records of that range go, in any order, to
+// [tile_base[t] + pre[g0][t], ...) -- exactly where the per-(slab, tile)
+// segments g0..g1-1 of the final layout lie.
 __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out1, uint32_t F, int G,
                                                 const uint32_t* __restrict__ pre,
-                                                const uint32_t* __restrict__ tile_tot,
-                                                const uint32_t* __restrict__ tile_base, Tables tb,
+                                                const uint32_t* __restrict__ tile_base,
+                                                const uint32_t* __restrict__ plan, Tables tb,
                                                 uint32_t* __restrict__ records) {
   __shared__ int32_t lim[LIM_PAD];
   __shared__ uint16_t lut[LUT_N];
-  __shared__ uint32_t cur[B2_GBLK][ST_TILES];
-  __shared__ uint32_t seg[B2_GBLK + 1];
+  __shared__ uint32_t cur[ST_TILES];      // global write position of each tile
+  __shared__ uint32_t cnt[ST_TILES];      // records of each tile in this sub-chunk
+  __shared__ uint32_t off[ST_TILES];      // their exclusive offsets in stage
+  __shared__ uint32_t stage[CH2];         // sub-chunk records sorted by tile
+  __shared__ uint8_t stage_tl[CH2];
+  __shared__ uint32_t seg[2];
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t item = blockIdx.x;
+  if (item >= plan[FS]) return;
+  uint32_t lo = 0, hi = FS;  // last j with plan[j] <= item
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (plan[m] <= item) lo = m; else hi = m;
+  }
+  const uint32_t j = lo;
+  const uint32_t gsz = plan[FS + 1 + j];
+  const int g0 = (int)((item - plan[j]) * gsz);
+  const int g1 = min(G, g0 + (int)gsz);
   for (int i = threadIdx.x; i < LIM_PAD; i += B2_NT) lim[i] = tb.lim_pad[i];
   for (int i = threadIdx.x; i < LUT_N; i += B2_NT) lut[i] = tb.lut[i];
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t j = blockIdx.x % FS;
-  const int g0 = (int)(blockIdx.x / FS) * B2_GBLK;
-  const int ng = min(B2_GBLK, G - g0);
   const uint32_t t0 = j * ST_TILES;
   const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  // cursors of the block's slabs; segment lengths
-  for (int gi = w; gi < B2_GBLK; gi += B2_NT / 64) {
-    uint32_t p = 0, c = 0;
-    if (gi < ng && (uint32_t)lane < nt) {
-      const int g = g0 + gi;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    uint32_t p0 = 0, p1 = 0;
+    if ((uint32_t)lane < nt) {
       const uint32_t t = t0 + lane;
-      p = pre[(size_t)g * F + t];
-      const uint32_t nxt = (g + 1 < G) ? pre[(size_t)(g + 1) * F + t] : tile_tot[t];
-      c = nxt - p;
-      cur[gi][lane] = tile_base[t] + p;
+      p0 = pre[(size_t)g0 * F + t];
+      p1 = g1 < G ? pre[(size_t)g1 * F + t] : (tile_base[t + 1] - tile_base[t]);
+      cur[lane] = tile_base[t] + p0;
     }
-    uint32_t sp = p, sc = c;
+    cnt[lane] = 0;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
-      sp += __shfl_xor(sp, d, 64);
-      sc += __shfl_xor(sc, d, 64);
+      p0 += __shfl_xor(p0, d, 64);
+      p1 += __shfl_xor(p1, d, 64);
     }
     if (lane == 0) {
-      if (gi == 0) seg[0] = tile_base[t0] + sp;
-      seg[gi + 1] = sc;  // length for now
+      seg[0] = tile_base[t0] + p0;
+      seg[1] = tile_base[t0] + p1;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t a = seg[0];
-    for (int gi = 0; gi < B2_GBLK; ++gi) {
-      a += seg[gi + 1];
-      seg[gi + 1] = a;  // end of segment gi
+  const uint32_t A = seg[0], B = seg[1];
+  const uint32_t A16 = A & ~3u;  // 16-B aligned start; lanes below A are masked off
+  constexpr int PT = CH2 / B2_NT;  // 16 records per thread: 4 x uint4
+  for (uint32_t c0 = A16; c0 < B; c0 += CH2) {
+    uint32_t rec[PT], tlv[PT], rank[PT];
+#pragma unroll
+    for (int k = 0; k < PT / 4; ++k) {
+      const uint32_t base = c0 + 4 * (k * B2_NT + threadIdx.x);
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      if (base < B) x = *reinterpret_cast<const uint4*>(out1 + base);  // out1 padded to a multiple of 4
+      const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t idx = base + e;
+        const bool valid = idx >= A && idx < B;
+        const uint32_t r = xv[e];
+        const uint32_t tl = r >> 26;
+        const uint32_t loc = (r >> 21) & 31u;
+        const uint32_t pl = r & 0x1FFFFFu;
+        uint32_t b = 0, o = 0;
+        if (valid) {
+          if (pl < V_ESC) {
+            b = bucket_lut(pl, lut, lim);
+            o = pl - (b ? (uint32_t)lim[b - 1] : 0u);  // bucket width < 2^16 below V_ESC
+          } else {
+            b = pl - V_ESC;
+            o = OFF_ESC;
+          }
+        }
+        rec[4 * k + e] = (loc << 27) | (b << 16) | o;
+        tlv[4 * k + e] = valid ? tl : 0xFFu;
+        rank[4 * k + e] = wave_atomic_rank<3>(cnt, tl, valid);
+      }
     }
-  }
-  __syncthreads();
-  const uint32_t A = seg[0];
-  const uint32_t B = seg[B2_GBLK];
-  int gi = 0;
-  auto one = [&](uint32_t idx, uint32_t r) {
-    while (idx >= seg[gi + 1]) ++gi;  // indices only grow per thread
-    const uint32_t tl = r >> 26;
-    const uint32_t loc = (r >> 21) & 31u;
-    const uint32_t pl = r & 0x1FFFFFu;
-    uint32_t b, off;
-    if (pl < V_ESC) {
-      b = bucket_lut(pl, lut, lim);
-      off = pl - (b ? (uint32_t)lim[b - 1] : 0u);  // bucket width < 2^16 below V_ESC
-    } else {
-      b = pl - V_ESC;
-      off = OFF_ESC;
+    __syncthreads();
+    uint32_t total = 0;
+    if (threadIdx.x < 64) {  // exclusive scan of the 64 tile counts (one wave)
+      const uint32_t v = cnt[threadIdx.x];
+      uint32_t x = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if ((int)threadIdx.x >= d) x += y;
+      }
+      off[threadIdx.x] = x - v;
     }
-    records[atomicAdd(&cur[gi][tl], 1u)] = (loc << 27) | (b << 16) | off;
-  };
-  // flat range [A, B): head to 16-B alignment, then 2 x uint4 per thread per step
-  const uint32_t A4 = min(B, (A + 3u) & ~3u);
-  if (A + threadIdx.x < A4) one(A + threadIdx.x, out1[A + threadIdx.x]);
-  const uint32_t nv = (B - A4) >> 2;
-  const uint4* __restrict__ p = reinterpret_cast<const uint4*>(out1 + A4);
-  uint32_t i = threadIdx.x;
-  for (; i + B2_NT < nv; i += 2 * B2_NT) {
-    const uint4 x = p[i];
-    const uint4 y = p[i + B2_NT];
-    const uint32_t bx = A4 + 4 * i, by = A4 + 4 * (i + B2_NT);
-    one(bx, x.x); one(bx + 1, x.y); one(bx + 2, x.z); one(bx + 3, x.w);
-    one(by, y.x); one(by + 1, y.y); one(by + 2, y.z); one(by + 3, y.w);
-  }
-  if (i < nv) {
-    const uint4 x = p[i];
-    const uint32_t bx = A4 + 4 * i;
-    one(bx, x.x); one(bx + 1, x.y); one(bx + 2, x.z); one(bx + 3, x.w);
-  }
-  const uint32_t tt = A4 + (nv << 2) + threadIdx.x;
-  if (tt < B) {
-    gi = 0;
-    one(tt, out1[tt]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      if (tlv[k] != 0xFFu) {
+        const uint32_t pos = off[tlv[k]] + rank[k];
+        stage[pos] = rec[k];
+        stage_tl[pos] = (uint8_t)tlv[k];
+      }
+    }
+    total = off[ST_TILES - 1] + cnt[ST_TILES - 1];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += B2_NT) {
+      const uint32_t tl = stage_tl[i];
+      records[cur[tl] + (i - off[tl])] = stage[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      cur[threadIdx.x] += cnt[threadIdx.x];
+      cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -423,11 +493,15 @@ hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, si
   return hipGetLastError();
 }
 
-hipError_t launch_bin2(const uint32_t* scratch1, int G, uint32_t F, const uint32_t* pre, const uint32_t* tile_tot,
-                       const uint32_t* tile_base, Tables tb, uint32_t* records, hipStream_t st) {
+hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
+                       const uint32_t* tile_tot, const uint32_t* tile_base, Tables tb, uint32_t* plan,
+                       uint32_t* records, hipStream_t st) {
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const int nb = (G + B2_GBLK - 1) / B2_GBLK;
-  hipLaunchKernelGGL(k_bin2, dim3(FS * nb), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_tot, tile_base, tb,
+  hipLaunchKernelGGL(k_bin2plan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, plan);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t max_items = n / B2_ITEM + FS + 1;  // sum_j ceil(tot_j / B2_ITEM)
+  hipLaunchKernelGGL(k_bin2, dim3((unsigned)max_items), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_base, plan, tb,
                      records);
   return hipGetLastError();
 }

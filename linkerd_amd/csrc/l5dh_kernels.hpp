@@ -57,9 +57,10 @@ struct State {
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
-  uint32_t* item_start;    // [F+1]
-  uint32_t* hot_list;      // [F]
-  uint32_t* header;        // [4] total items, hot tiles
+  uint32_t* item_start;    // [F+1] cold items (one per cold tile)
+  uint32_t* item_start2;   // [F+1] warm/hot items (one per hot_chunk records)
+  uint32_t* hot_list;      // [F] multi-chunk tiles
+  uint32_t* header;        // [4] cold items, multi-chunk tiles, warm/hot items
 };
 
 struct Outputs {
@@ -82,13 +83,16 @@ constexpr size_t BIN1_LDS = (size_t)8192 * 4 + 8192 * 2 + 3 * 512 * 4;
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, uint32_t* scratch1,
                        int64_t* sumfix, bool vec, hipStream_t st);
-hipError_t launch_bin2(const uint32_t* scratch1, int G, uint32_t F, const uint32_t* pre, const uint32_t* tile_tot,
-                       const uint32_t* tile_base, Tables tb, uint32_t* records, hipStream_t st);
+// plan: device scratch of >= 2*FS + 2 u32 (FS = ceil(F/64) <= 512)
+hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
+                       const uint32_t* tile_tot, const uint32_t* tile_base, Tables tb, uint32_t* plan,
+                       uint32_t* records, hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
                        hipStream_t st);
 hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st);
-hipError_t launch_accum(Segs segs, Plan plan, uint32_t num_items, State state, Tables tb, Outputs out,
-                        uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset, hipStream_t st);
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
+                        Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
+                        hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
                              int reset, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external

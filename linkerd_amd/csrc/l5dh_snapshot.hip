@@ -19,9 +19,10 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
                                                uint32_t hot_chunk, Plan plan) {
   __shared__ uint32_t lds_a[17];
   __shared__ uint32_t lds_b[17];
+  __shared__ uint32_t lds_c[17];
   const uint32_t per = (F + 1023) / 1024;
   const uint32_t t0 = threadIdx.x * per;
-  uint32_t items = 0, hot = 0;
+  uint32_t ci = 0, hi = 0, hot = 0;  // cold items, warm/hot items, multi-chunk tiles
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t t = t0 + k;
     if (t >= F) break;
@@ -29,31 +30,35 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
     plan.tile_tot[t] = tot;
     if (tot > cold_limit) {
-      items += 2u * ((tot + hot_chunk - 1) / hot_chunk);
-      hot += 1;
+      hi += (tot + hot_chunk - 1) / hot_chunk;
+      hot += tot > hot_chunk ? 1u : 0u;
     } else if (final_mode || tot > 0) {
-      items += 1;
+      ci += 1;
     }
   }
-  uint32_t tot_items, tot_hot;
-  uint32_t ia = block_excl_scan<1024>(items, lds_a, &tot_items);
-  uint32_t ha = block_excl_scan<1024>(hot, lds_b, &tot_hot);
+  uint32_t tot_c, tot_h, tot_hot;
+  uint32_t ca = block_excl_scan<1024>(ci, lds_a, &tot_c);
+  uint32_t ha = block_excl_scan<1024>(hi, lds_b, &tot_h);
+  uint32_t xa = block_excl_scan<1024>(hot, lds_c, &tot_hot);
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t t = t0 + k;
     if (t >= F) break;
     const uint32_t tot = plan.tile_tot[t];
-    plan.item_start[t] = ia;
+    plan.item_start[t] = ca;
+    plan.item_start2[t] = ha;
     if (tot > cold_limit) {
-      ia += 2u * ((tot + hot_chunk - 1) / hot_chunk);
-      plan.hot_list[ha++] = t;
+      ha += (tot + hot_chunk - 1) / hot_chunk;
+      if (tot > hot_chunk) plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
-      ia += 1;
+      ca += 1;
     }
   }
   if (threadIdx.x == 0) {
-    plan.item_start[F] = tot_items;
-    plan.header[0] = tot_items;
+    plan.item_start[F] = tot_c;
+    plan.item_start2[F] = tot_h;
+    plan.header[0] = tot_c;
     plan.header[1] = tot_hot;
+    plan.header[2] = tot_h;
   }
 }
 
@@ -80,22 +85,112 @@ __device__ __forceinline__ uint32_t find_tile(const uint32_t* __restrict__ item_
   return lo;
 }
 
-// k_accum: one work item = one tile (cold: <= cold_limit records, 32 series in
-// u16-packed LDS bins, fused summary + dense flush) or one (tile, half, chunk)
-// of a hot tile (16 series in u32 LDS bins, flushed with global atomics).
-__global__ __launch_bounds__(WG) void k_accum(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+struct SrcLds32 {  // u32 row in LDS (warm/hot half-tiles), bins 1798/1799 zero
+  const uint32_t* row;
+  __device__ __forceinline__ uint4 get4(int b0) const { return *reinterpret_cast<const uint4*>(row + b0); }
+};
+
+// One series of a tile whose new-record counts sit in LDS (`lds`, u16 or u32
+// row) and whose exact offset sum is `offs`: merge with the old state if the
+// tile is dirty, write the dense row(s), fold sumfix into the total and, in a
+// final snapshot, emit the HistogramSummary.  One wave.
+template <class SrcL>
+__device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_t offs, bool dirty, bool keep,
+                                            int final_mode, State st, Tables tb, Outputs out) {
+  const int lane = lane_id();
+  const int ng = lane_groups(lane);
+  const uint32_t oi = s - out.first;
+  const bool emit = final_mode && s >= out.first && oi < out.count;
+  int32_t* orow = (emit && out.counts) ? out.counts + (size_t)oi * NB : nullptr;
+  uint32_t* srow = st.counts + (size_t)s * ROW;
+  uint32_t g[9];
+  uint64_t bs = 0;  // sum_b newcount_b * base_b (+ offs) = exact sum of the new samples
+  if (!dirty) {
+    // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are padding)
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) {
+      const int q = lane + 64 * k;
+      if (q < NB4) {
+        const int b0 = 4 * q;
+        const uint4 v = lds.get4(b0);
+        bs += dot4(v, tb.base, b0);
+        if (orow) store4_1798(orow, b0, v);
+        if (keep) store4_state(srow, b0, v);
+      }
+    }
+    // blocked group sums for the summary scan
+#pragma unroll
+    for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
+  } else {
+    const SrcRow32 old{srow};
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      g[q] = 0;
+      if (q < ng) {
+        const int b0 = 28 * lane + 4 * q;
+        const uint4 v = lds.get4(b0);
+        bs += dot4(v, tb.base, b0);
+        const uint4 o = old.get4(b0);
+        const uint4 cmb = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+        g[q] = sum4(cmb);
+        if (orow) store4_1798(orow, b0, cmb);
+        store4_state(srow, b0, cmb);  // the merged row is also the summary source
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  }
+  bs = wave_sum(bs);
+  int64_t total = (int64_t)(bs + offs) + st.sumfix[s];
+  if (dirty) total += st.total[s];
+  if (lane == 0) {
+    st.sumfix[s] = 0;
+    if (keep) st.total[s] = total;
+  }
+  if (emit) {
+    Summary88* so = out.summ ? out.summ + oi : nullptr;
+    if (dirty)
+      wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
+    else
+      wave_summary(g, lds, total, tb.mid, so);
+  }
+}
+
+// Records of tile t in the virtual range [vlo, vhi) of its concatenated segments.
+template <class Fn>
+__device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi, Fn&& fn) {
+  uint64_t vbase = 0;
+  for (int j = 0; j < segs.n; ++j) {
+    const uint32_t a = segs.tbase[j][t];
+    const uint32_t e = segs.tbase[j][t + 1];
+    const uint64_t len = e - a;
+    const uint64_t lo = vlo > vbase ? vlo : vbase;
+    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+    if (lo < hi) {
+      const uint32_t ra = a + (uint32_t)(lo - vbase);
+      for_records<WG>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), fn);
+    }
+    vbase += len;
+  }
+}
+
+// k_accum: one work item =
+//   cold tile (<= cold_limit records): 32 series in u16-packed LDS bins, one pass;
+//   warm tile (<= hot_chunk records): two rounds (series 0-15, 16-31) in u32 LDS
+//     bins over the same records (the second read hits L2), outputs in place;
+//   hot chunk (hot_chunk records of a bigger tile): the same two rounds, each
+//     flushed with global atomics into the state rows (k_hot_finish completes).
+__global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                               uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t item = blockIdx.x;
   const uint32_t F = st.F;
   const uint32_t t = find_tile(plan.item_start, F, item);
-  const uint32_t sub = item - plan.item_start[t];
   const uint32_t tot = plan.tile_tot[t];
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
+  const bool keep = !(final_mode && reset);
 
-  if (tot <= cold_limit) {
-    // ---------------- cold tile: single pass ----------------
+  {
     uint32_t* hist = smem;                    // [32][900] u16 pairs
     uint32_t* offsum = smem + TILE * CROW;    // [32]
     {
@@ -104,135 +199,88 @@ __global__ __launch_bounds__(WG) void k_accum(Segs segs, Plan plan, State st, Ta
       if (threadIdx.x < TILE) offsum[threadIdx.x] = 0;
     }
     __syncthreads();
-    for (int j = 0; j < segs.n; ++j) {
-      for_records<WG>(segs.recs[j], segs.tbase[j][t], segs.tbase[j][t + 1], [&](uint32_t rec) {
-        const uint32_t loc = rec >> 27;
-        const uint32_t b = (rec >> 16) & 0x7FFu;
-        const uint32_t off = rec & 0xFFFFu;
-        atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-        if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[loc], off);
-      });
-    }
+    for_tile_records(segs, t, 0, tot, [&](uint32_t rec) {
+      const uint32_t loc = rec >> 27;
+      const uint32_t b = (rec >> 16) & 0x7FFu;
+      const uint32_t off = rec & 0xFFFFu;
+      atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+      if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[loc], off);
+    });
     __syncthreads();
     const bool dirty = st.dirty[t] != 0;
-    const bool keep = !(final_mode && reset);
-    const int ng = lane_groups(lane);
     for (int rep = 0; rep < 2; ++rep) {
       const uint32_t loc = w + 16 * rep;
       const uint32_t s = t * TILE + loc;
       if (s >= st.S) continue;
-      const uint32_t oi = s - out.first;
-      const bool emit = final_mode && s >= out.first && oi < out.count;
-      int32_t* orow = (emit && out.counts) ? out.counts + (size_t)oi * NB : nullptr;
-      uint32_t* srow = st.counts + (size_t)s * ROW;
-      const SrcLds16 lds{hist + loc * CROW};
-      uint32_t g[9];
-      uint64_t bs = 0;  // sum_b newcount_b * base_b (+ sum(off) below) = exact sum of new samples
-      if (!dirty) {
-        // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are LDS padding)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int q = lane + 64 * k;
-          if (q < NB4) {
-            const int b0 = 4 * q;
-            const uint4 v = lds.get4(b0);
-            bs += dot4(v, tb.base, b0);
-            if (orow) store4_1798(orow, b0, v);
-            if (keep) store4_state(srow, b0, v);
-          }
-        }
-        // blocked group sums for the summary scan
-#pragma unroll
-        for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
-      } else {
-        const SrcRow32 old{srow};
-#pragma unroll
-        for (int q = 0; q < 9; ++q) {
-          g[q] = 0;
-          if (q < ng) {
-            const int b0 = 28 * lane + 4 * q;
-            const uint4 v = lds.get4(b0);
-            bs += dot4(v, tb.base, b0);
-            const uint4 o = old.get4(b0);
-            const uint4 cmb = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
-            g[q] = sum4(cmb);
-            if (orow) store4_1798(orow, b0, cmb);
-            store4_state(srow, b0, cmb);  // the merged row is also the summary source
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      }
-      bs = wave_sum(bs);
-      int64_t total = (int64_t)bs + (int64_t)offsum[loc] + st.sumfix[s];
-      if (dirty) total += st.total[s];
-      if (lane == 0) {
-        st.sumfix[s] = 0;
-        if (keep) st.total[s] = total;
-      }
-      if (emit) {
-        Summary88* so = out.summ ? out.summ + oi : nullptr;
-        if (dirty)
-          wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
-        else
-          wave_summary(g, lds, total, tb.mid, so);
-      }
+      emit_series(SrcLds16{hist + loc * CROW}, s, offsum[loc], dirty, keep, final_mode, st, tb, out);
     }
-    if (threadIdx.x == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
-  } else {
-    // ---------------- hot tile: split over (half, chunk) ----------------
-    uint32_t* hist = smem;                                                   // [16][1800] u32
-    unsigned long long* offsum = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16]
-    const uint32_t half = sub & 1u;
-    const uint32_t chunk = sub >> 1;
+    if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
+  }
+
+}
+
+__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                              uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t item = blockIdx.x;
+  const uint32_t F = st.F;
+  const uint32_t t = find_tile(plan.item_start2, F, item);
+  const uint32_t sub = item - plan.item_start2[t];
+  const uint32_t tot = plan.tile_tot[t];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const bool keep = !(final_mode && reset);
+
+  // warm tile or hot chunk: two rounds of 16 series in u32 LDS bins
+  uint32_t* hist = smem;                                                                 // [16][1800]
+  unsigned long long* offsum = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16]
+  const bool single = tot <= hot_chunk;
+  const bool dirty = single && st.dirty[t] != 0;
+  const uint64_t vlo = (uint64_t)sub * hot_chunk;
+  const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
+#pragma unroll 1
+  for (uint32_t half = 0; half < 2; ++half) {
     {
       uint4* p = reinterpret_cast<uint4*>(smem);
       for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
       if (threadIdx.x < 16) offsum[threadIdx.x] = 0;
     }
     __syncthreads();
-    const uint64_t vlo = (uint64_t)chunk * hot_chunk;
-    const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
-    uint64_t vbase = 0;
-    for (int j = 0; j < segs.n; ++j) {
-      const uint32_t a = segs.tbase[j][t];
-      const uint32_t e = segs.tbase[j][t + 1];
-      const uint64_t len = e - a;
-      const uint64_t lo = vlo > vbase ? vlo : vbase;
-      const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
-      if (lo < hi) {
-        const uint32_t ra = a + (uint32_t)(lo - vbase);
-        for_records<WG>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), [&](uint32_t rec) {
-          const uint32_t loc = rec >> 27;
-          if ((loc >> 4) != half) return;
-          const uint32_t l = loc & 15u;
-          const uint32_t b = (rec >> 16) & 0x7FFu;
-          const uint32_t off = rec & 0xFFFFu;
-          atomicAdd(&hist[l * HROW + b], 1u);
-          if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
-        });
-      }
-      vbase += len;
-    }
+    for_tile_records(segs, t, vlo, vhi, [&](uint32_t rec) {
+      const uint32_t loc = rec >> 27;
+      if ((loc >> 4) != half) return;
+      const uint32_t l = loc & 15u;
+      const uint32_t b = (rec >> 16) & 0x7FFu;
+      const uint32_t off = rec & 0xFFFFu;
+      atomicAdd(&hist[l * HROW + b], 1u);
+      if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
+    });
     __syncthreads();
     const uint32_t s = t * TILE + 16 * half + w;
     if (s < st.S) {
-      uint32_t* grow = st.counts + (size_t)s * ROW;
-      const uint32_t* hrow = hist + w * HROW;
-      uint64_t bs = 0;
-      for (int b = lane; b < NB; b += 64) {
-        const uint32_t v = hrow[b];
-        if (v) {
-          bs += (uint64_t)v * (uint64_t)(uint32_t)tb.base[b];
-          atomicAdd(&grow[b], v);
+      if (single) {
+        emit_series(SrcLds32{hist + w * HROW}, s, offsum[w], dirty, keep, final_mode, st, tb, out);
+      } else {
+        uint32_t* grow = st.counts + (size_t)s * ROW;
+        const uint32_t* hrow = hist + w * HROW;
+        uint64_t bs = 0;
+        for (int b = lane; b < NB; b += 64) {
+          const uint32_t v = hrow[b];
+          if (v) {
+            bs += (uint64_t)v * (uint64_t)(uint32_t)tb.base[b];
+            atomicAdd(&grow[b], v);
+          }
+        }
+        bs = wave_sum(bs);
+        if (lane == 0) {
+          const uint64_t add = bs + offsum[w];
+          if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
         }
       }
-      bs = wave_sum(bs);
-      if (lane == 0) {
-        const uint64_t add = bs + offsum[w];
-        if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
-      }
     }
+    __syncthreads();
   }
+  if (single && threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
 }
 
 // k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
@@ -315,7 +363,9 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
 }  // namespace
 
 hipError_t set_snapshot_attributes() {
-  return hipFuncSetAttribute((const void*)k_accum, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
@@ -330,12 +380,21 @@ hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t
   return hipGetLastError();
 }
 
-hipError_t launch_accum(Segs segs, Plan plan, uint32_t num_items, State state, Tables tb, Outputs out,
-                        uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset, hipStream_t st) {
-  if (num_items == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_accum, dim3(num_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
-                     hot_chunk, final_mode, reset);
-  return hipGetLastError();
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
+                        Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
+                        hipStream_t st) {
+  if (cold_items) {
+    hipLaunchKernelGGL(k_accum_cold, dim3(cold_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
+                       hot_chunk, final_mode, reset);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (hot_items) {
+    hipLaunchKernelGGL(k_accum_hot, dim3(hot_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
+                       hot_chunk, final_mode, reset);
+    return hipGetLastError();
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,

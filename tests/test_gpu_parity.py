@@ -114,15 +114,16 @@ def test_multi_batch_and_cumulative_snapshots(oracle, reset):
 
 @BIN_MODES
 def test_hot_tile_split_path(oracle, bin_mode):
-    """Force the split (hot-tile) path: small cold limit and chunk."""
+    """Warm tiles (cold_limit < records <= hot_chunk: two u32 half-rounds, outputs in
+    place) and hot tiles (> hot_chunk: chunk items + global atomics + k_hot_finish)."""
     rng = np.random.default_rng(9)
     S = 100
     eng = _engine(S, bin_mode)
     eng.set_param(N.PARAM_COLD_LIMIT, 500)
-    eng.set_param(N.PARAM_HOT_CHUNK, 1024)
+    eng.set_param(N.PARAM_HOT_CHUNK, 65536)
     o = oracle.OracleHistograms(S)
-    # skewed: series 0..3 hot
-    series = np.concatenate([rng.integers(0, 4, 40000), rng.integers(0, S, 5000)]).astype(np.uint32)
+    # series 0..3 (tile 0) hot: 3+ chunks; tiles 1..3 warm; a few cold-ish
+    series = np.concatenate([rng.integers(0, 4, 200_000), rng.integers(32, S, 20_000)]).astype(np.uint32)
     vals = np.exp(3 + rng.standard_normal(series.size)).astype(np.float32)
     vals[::97] = rng.choice(EDGE_VALUES, size=vals[::97].size)
     eng.ingest(series, vals)
@@ -131,11 +132,16 @@ def test_hot_tile_split_path(oracle, bin_mode):
     np.testing.assert_array_equal(counts, o.counts())
     _assert_summaries_equal(got, o.snapshot(reset=False), "hot1")
     # second round on top of dirty state, then reset
-    eng.ingest(series[:30000], vals[:30000])
-    o.ingest(series[:30000], vals[:30000])
+    eng.ingest(series[:150_000], vals[:150_000])
+    o.ingest(series[:150_000], vals[:150_000])
     got, counts = eng.snapshot(reset=True, with_counts=True)
     np.testing.assert_array_equal(counts, o.counts())
     _assert_summaries_equal(got, o.snapshot(reset=True), "hot2")
+    # and a fold (range snapshot) through the hot path
+    eng.ingest(series, vals)
+    o.ingest(series, vals)
+    got = eng.snapshot(first=0, count=40, reset=True)
+    _assert_summaries_equal(got, o.snapshot(reset=False)[:40], "hot fold")
 
 
 def test_range_snapshot_peek_export(oracle):

@@ -1,0 +1,45 @@
+"""Aggregate rocprofv3 --pmc CSVs (tools/profile_pmc.sh) per kernel: average value
+of each counter per dispatch, HBM bytes per launch with the gfx950 corrections of
+MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of wide streaming reads:
+doubled; WRITE_SIZE taken as is; both in KB)."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"k_[a-z0-9_]+", name)
+    return m.group(0)[2:] if m else name[:40]
+
+
+def main(d, out_json=None, meta=None):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r.get("Kernel_Name", ""))
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {}
+    for k, cs in sorted(acc.items()):
+        row = {c: sum(v) / len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in row or "WRITE_SIZE" in row:
+            rd = 2 * 1024 * row.get("FETCH_SIZE", 0.0)
+            wr = 1024 * row.get("WRITE_SIZE", 0.0)
+            row["hbm_read_bytes_per_launch"] = rd
+            row["hbm_write_bytes_per_launch"] = wr
+            row["hbm_bytes_per_launch"] = rd + wr
+        res[k] = row
+    for k, row in res.items():
+        print(k, json.dumps({c: (round(v / 1e6, 2) if "bytes" in c else round(v)) for c, v in row.items()}))
+    if out_json:
+        doc = dict(meta or {})
+        doc["kernels"] = res
+        json.dump(doc, open(out_json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    meta = json.loads(sys.argv[3]) if len(sys.argv) > 3 else None
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None, meta)
