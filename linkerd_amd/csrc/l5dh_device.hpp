@@ -339,6 +339,35 @@ __device__ __forceinline__ void wave_atomic_inc(uint32_t* ctr, uint32_t key, boo
   if (!done) atomicAdd(&ctr[key], 1u);
 }
 
+// Rank of this lane's increment of ctr[key] (like atomicAdd(&ctr[key], 1)); lanes
+// whose key is one of the wave-uniform hot keys (Zipf heads, found exactly from
+// the count pass) are merged into one atomic per hot key.  Convergent.
+__device__ __forceinline__ uint32_t hot_rank(uint32_t* ctr, uint32_t key, bool valid, uint32_t hot0,
+                                             uint32_t hot1) {
+  uint32_t rank = 0;
+  bool handled = !valid;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t hk = h ? hot1 : hot0;
+    if (hk != 0xFFFFFFFFu) {
+      const bool mine = valid && key == hk;
+      const unsigned long long m = __ballot(mine);
+      if (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&ctr[hk], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (mine) {
+          rank = base + mask_below(m);
+          handled = true;
+        }
+      }
+    }
+  }
+  if (!handled) rank = atomicAdd(&ctr[key], 1u);
+  return rank;
+}
+
 // Visit records r[a, e) with 16-B loads, two in flight per thread per step.
 template <int NT, class Fn>
 __device__ __forceinline__ void for_records(const uint32_t* __restrict__ r, uint32_t a, uint32_t e, Fn&& fn) {

@@ -359,13 +359,17 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     int r = ensure(c, c->scratch1, n * 4 + 16);  // k_bin2 reads whole 16-B groups
     if (r) return r;
     {
+      KTimer kt(c, L5DH_K_SCAN);
+      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, c->stream));
+    }
+    {
       KTimer kt(c, L5DH_K_BIN);
-      HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
+      HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
                             static_cast<uint32_t*>(c->scratch1.p), c->d_sumfix, vec, c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
-    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, c->d_tile_tot, sg.tbase,
-                          tables(c), c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->stream));
+    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, tables(c),
+                          c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->stream));
   } else {
     KTimer kt(c, L5DH_K_BIN);
     HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
@@ -476,7 +480,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
             mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
-            mal((void**)&c->d_b2plan, 4 * 1026);
+            mal((void**)&c->d_b2plan, 4 * 2048);
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
   if (!ok) {
     (void)hipGetLastError();

@@ -210,7 +210,8 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
-                                                uint32_t* __restrict__ out1, int64_t* __restrict__ sumfix, int vec) {
+                                                const uint32_t* __restrict__ stplan, uint32_t* __restrict__ out1,
+                                                int64_t* __restrict__ sumfix, int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t lds9[B1_NT / 64 + 1];
   uint32_t* stage = smem;                                         // [CH1]
@@ -219,6 +220,7 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   uint32_t* stoff = stcnt + FS_MAX;
   uint32_t* stcur = stoff + FS_MAX;
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t hot0 = stplan[3 * FS + 1], hot1 = stplan[3 * FS + 2];
   const uint32_t* prow = pre + (size_t)blockIdx.x * F;
   for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
     const uint32_t t0 = j * ST_TILES;
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
         rec[k] = (((s >> TILE_SHIFT) & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl;
         stv[k] = s >> ST_SHIFT;
       }
-      rank[k] = wave_atomic_rank<3>(stcnt, ok ? stv[k] : 0u, ok);
+      rank[k] = hot_rank(stcnt, ok ? stv[k] : 0u, ok, hot0, hot1);
     }
     __syncthreads();
     uint32_t tot;
@@ -296,19 +298,34 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   }
 }
 
-// Level-2 plan (one workgroup): per super-tile j, nb_j items of equal slab
-// ranges so that every item holds about B2_ITEM records (skew-balanced).
-// plan[0..FS] = item_start, plan[FS+1 .. 2FS] = slab range size per ST.
-__global__ __launch_bounds__(1024) void k_bin2plan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
-                                                   uint32_t* __restrict__ plan) {
+// Super-tile plan (one workgroup, after the tile totals are known):
+//   plan[0..FS]          level-2 item_start per super-tile (nb_j items of equal
+//                        slab ranges, ~B2_ITEM records each: skew-balanced)
+//   plan[FS+1 .. 2FS]    slab-range size per super-tile
+//   plan[2FS+1 .. 3FS]   hot tiles of the super-tile (tile-in-ST, byte 0 and 1;
+//                        0xFF = none): tiles holding >= 1/8 of its records
+//   plan[3FS+1], [3FS+2] hot super-tiles: >= 1/8 of all records (or ~0u)
+constexpr uint32_t NOKEY = 0xFFFFFFFFu;
+__global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
+                                                 uint32_t* __restrict__ plan) {
   __shared__ uint32_t lds[17];
+  __shared__ unsigned long long best[16];
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  uint32_t nb = 0, gsz = 0;
+  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu;
+  uint64_t tot = 0;
   const uint32_t j = threadIdx.x;
   if (j < FS) {
-    uint64_t tot = 0;
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    for (uint32_t t = j * ST_TILES; t < t1; ++t) tot += tile_tot[t];
+    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;
+    for (uint32_t t = j * ST_TILES; t < t1; ++t) {
+      const uint32_t v = tile_tot[t];
+      tot += v;
+      if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = t - j * ST_TILES; }
+      else if (v > b1) { b1 = v; i1 = t - j * ST_TILES; }
+    }
+    if ((uint64_t)b0 * 8 < tot || b0 == 0) i0 = 0xFF;
+    if ((uint64_t)b1 * 8 < tot || b1 == 0) i1 = 0xFF;
+    hot = i0 | (i1 << 8);
     uint32_t want = (uint32_t)((tot + B2_ITEM - 1) / B2_ITEM);
     want = max(1u, min(want, (uint32_t)G));
     gsz = ((uint32_t)G + want - 1) / want;
@@ -319,8 +336,35 @@ __global__ __launch_bounds__(1024) void k_bin2plan(uint32_t F, int G, const uint
   if (j < FS) {
     plan[j] = e;
     plan[FS + 1 + j] = gsz;
+    plan[2 * FS + 1 + j] = hot;
   }
   if (threadIdx.x == 0) plan[FS] = total;
+  // grand total and the two biggest super-tiles (key = tot << 10 | j), block reductions
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  auto block_reduce = [&](unsigned long long v, bool is_max) -> unsigned long long {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const unsigned long long o = __shfl_xor(v, d, 64);
+      v = is_max ? (o > v ? o : v) : v + o;
+    }
+    __syncthreads();
+    if (lane == 0) best[w] = v;
+    __syncthreads();
+    unsigned long long r = 0;
+    for (int q = 0; q < 16; ++q) r = is_max ? (best[q] > r ? best[q] : r) : r + best[q];
+    return r;
+  };
+  const unsigned long long grand = block_reduce(tot, false);
+  const unsigned long long key = j < FS ? ((tot << 10) | j) : 0ull;
+  const unsigned long long k1 = block_reduce(key, true);
+  const unsigned long long k2 = block_reduce(key == k1 ? 0ull : key, true);
+  if (threadIdx.x == 0) {
+    const unsigned long long ks[2] = {k1, k2};
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t v = ks[h] >> 10;
+      plan[3 * FS + 1 + h] = (v > 0 && v * 8 >= grand) ? (uint32_t)(ks[h] & 1023u) : NOKEY;
+    }
+  }
 }
 
 // Level 2.  Item = (super-tile j, slab range [g0, g1)).  Its level-1 records are
@@ -352,6 +396,9 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t gsz = plan[FS + 1 + j];
   const int g0 = (int)((item - plan[j]) * gsz);
   const int g1 = min(G, g0 + (int)gsz);
+  const uint32_t hp = plan[2 * FS + 1 + j];
+  const uint32_t hot0 = (hp & 0xFFu) == 0xFFu ? NOKEY : (hp & 0xFFu);
+  const uint32_t hot1 = ((hp >> 8) & 0xFFu) == 0xFFu ? NOKEY : ((hp >> 8) & 0xFFu);
   for (int i = threadIdx.x; i < LIM_PAD; i += B2_NT) lim[i] = tb.lim_pad[i];
   for (int i = threadIdx.x; i < LUT_N; i += B2_NT) lut[i] = tb.lut[i];
   const uint32_t t0 = j * ST_TILES;
@@ -380,13 +427,25 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t A = seg[0], B = seg[1];
   const uint32_t A16 = A & ~3u;  // 16-B aligned start; lanes below A are masked off
   constexpr int PT = CH2 / B2_NT;  // 16 records per thread: 4 x uint4
+  uint4 xn[PT / 4];                 // next sub-chunk, prefetched while this one is sorted and written
+#pragma unroll
+  for (int k = 0; k < PT / 4; ++k) {
+    const uint32_t base = A16 + 4 * (k * B2_NT + threadIdx.x);
+    xn[k] = base < B ? *reinterpret_cast<const uint4*>(out1 + base) : make_uint4(0u, 0u, 0u, 0u);
+  }
   for (uint32_t c0 = A16; c0 < B; c0 += CH2) {
     uint32_t rec[PT], tlv[PT], rank[PT];
+    uint4 xc[PT / 4];
+#pragma unroll
+    for (int k = 0; k < PT / 4; ++k) {
+      xc[k] = xn[k];
+      const uint32_t nbase = c0 + CH2 + 4 * (k * B2_NT + threadIdx.x);  // out1 padded to a multiple of 4
+      xn[k] = nbase < B ? *reinterpret_cast<const uint4*>(out1 + nbase) : make_uint4(0u, 0u, 0u, 0u);
+    }
 #pragma unroll
     for (int k = 0; k < PT / 4; ++k) {
       const uint32_t base = c0 + 4 * (k * B2_NT + threadIdx.x);
-      uint4 x = make_uint4(0u, 0u, 0u, 0u);
-      if (base < B) x = *reinterpret_cast<const uint4*>(out1 + base);  // out1 padded to a multiple of 4
+      const uint4 x = xc[k];
       const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -408,7 +467,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
         }
         rec[4 * k + e] = (loc << 27) | (b << 16) | o;
         tlv[4 * k + e] = valid ? tl : 0xFFu;
-        rank[4 * k + e] = wave_atomic_rank<3>(cnt, tl, valid);
+        rank[4 * k + e] = hot_rank(cnt, tl, valid, hot0, hot1);
       }
     }
     __syncthreads();
@@ -485,24 +544,26 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
   return hipGetLastError();
 }
 
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, hipStream_t st) {
+  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, stplan);
+  return hipGetLastError();
+}
+
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
-                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, uint32_t* scratch1,
-                       int64_t* sumfix, bool vec, hipStream_t st) {
+                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
+                       uint32_t* scratch1, int64_t* sumfix, bool vec, hipStream_t st) {
   hipLaunchKernelGGL(k_bin1, dim3(G), dim3(B1_NT), BIN1_LDS, st, series, values, n, per, S, F, pre, tile_base, tb,
-                     scratch1, sumfix, vec ? 1 : 0);
+                     stplan, scratch1, sumfix, vec ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
-                       const uint32_t* tile_tot, const uint32_t* tile_base, Tables tb, uint32_t* plan,
-                       uint32_t* records, hipStream_t st) {
+                       const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
+                       hipStream_t st) {
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  hipLaunchKernelGGL(k_bin2plan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, plan);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
   const size_t max_items = n / B2_ITEM + FS + 1;  // sum_j ceil(tot_j / B2_ITEM)
-  hipLaunchKernelGGL(k_bin2, dim3((unsigned)max_items), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_base, plan, tb,
-                     records);
+  hipLaunchKernelGGL(k_bin2, dim3((unsigned)max_items), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_base, stplan,
+                     tb, records);
   return hipGetLastError();
 }
 

@@ -80,13 +80,14 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
 // Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
 // (super-tile -> tiles).  scratch1 holds n level-1 records.
 constexpr size_t BIN1_LDS = (size_t)8192 * 4 + 8192 * 2 + 3 * 512 * 4;
+// Super-tile plan (level-2 items, hot keys); stplan: device scratch of 2048 u32.
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
-                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, uint32_t* scratch1,
-                       int64_t* sumfix, bool vec, hipStream_t st);
-// plan: device scratch of >= 2*FS + 2 u32 (FS = ceil(F/64) <= 512)
+                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
+                       uint32_t* scratch1, int64_t* sumfix, bool vec, hipStream_t st);
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
-                       const uint32_t* tile_tot, const uint32_t* tile_base, Tables tb, uint32_t* plan,
-                       uint32_t* records, hipStream_t st);
+                       const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
+                       hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
                        hipStream_t st);
 hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st);

@@ -186,7 +186,6 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
   const uint32_t F = st.F;
   const uint32_t t = find_tile(plan.item_start, F, item);
   const uint32_t tot = plan.tile_tot[t];
-  const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
 

@@ -1,0 +1,110 @@
+"""Multi-GPU layer: one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X; "gloo" for CPU tests).
+
+* Series sharding (config C3): series are independent, so each rank owns a
+  contiguous range of global series ids, balanced by (expected) sample counts;
+  ingest is routed by series and no collective touches the data path.
+* Fleet merge (config C4): samples of the same series space are spread over
+  ranks; each rank exports its dense int32 counts [S][1798] + int64 totals [S]
+  (l5dh_export_state), a reduce-scatter sums them (integer sums: bit-exact and
+  order independent) so rank r owns series slice r, which it summarizes with
+  l5dh_summarize_dense.  min/max are midpoints derived from counts, so they need
+  no separate min/max reduction.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+NB = 1798
+
+
+@dataclass(frozen=True)
+class Shard:
+    rank: int
+    first: int   # first global series id owned
+    count: int   # number of series owned
+
+
+def shard_ranges(total_series: int, world: int, weights: Optional[np.ndarray] = None) -> List[Shard]:
+    """Contiguous series ranges, balanced by weights (e.g. last interval's per-series
+    sample counts) when given, else by series count."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    if weights is None:
+        bounds = [(total_series * r) // world for r in range(world + 1)]
+    else:
+        w = np.asarray(weights, dtype=np.float64)
+        if w.size != total_series:
+            raise ValueError("weights must have one entry per series")
+        c = np.concatenate([[0.0], np.cumsum(w)])
+        targets = c[-1] * np.arange(world + 1) / world
+        bounds = np.searchsorted(c, targets, side="left").tolist()
+        bounds[0], bounds[-1] = 0, total_series
+        for r in range(1, world + 1):  # monotone, every rank may own zero or more
+            bounds[r] = max(bounds[r], bounds[r - 1])
+    return [Shard(r, bounds[r], bounds[r + 1] - bounds[r]) for r in range(world)]
+
+
+class SeriesRouter:
+    """Routes a COO batch of global series ids to the owning ranks (local ids)."""
+
+    def __init__(self, shards: Sequence[Shard]):
+        self.shards = list(shards)
+        self.starts = np.array([s.first for s in self.shards] + [self.shards[-1].first + self.shards[-1].count],
+                               dtype=np.int64)
+
+    def route(self, series: np.ndarray, values: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
+        series = np.asarray(series, dtype=np.int64)
+        owner = np.searchsorted(self.starts, series, side="right") - 1
+        out = []
+        for sh in self.shards:
+            m = owner == sh.rank
+            out.append(((series[m] - sh.first).astype(np.uint32), np.asarray(values)[m].astype(np.float32)))
+        return out
+
+
+def padded_rows(S: int, world: int) -> int:
+    return ((S + world - 1) // world) * world
+
+
+def fleet_merge(counts, totals, group=None, mode: str = "reduce_scatter"):
+    """Sum per-rank dense state across ranks.
+
+    counts: torch int32 [S][1798], totals: torch int64 [S] (same S on every rank;
+    device tensors with RCCL, CPU tensors with gloo).  Returns (counts_slice,
+    totals_slice, first): the rows this rank owns after the merge (all rows for
+    mode="all_reduce")."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S = counts.shape[0]
+    if mode == "all_reduce":
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
+        return counts, totals, 0
+    if mode != "reduce_scatter":
+        raise ValueError(f"unknown merge mode {mode!r}")
+    Sp = padded_rows(S, world)
+    per = Sp // world
+    if Sp != S:
+        counts = torch.cat([counts, counts.new_zeros((Sp - S, NB))])
+        totals = torch.cat([totals, totals.new_zeros(Sp - S)])
+    if dist.get_backend(group) == "gloo":
+        # gloo has no reduce_scatter: all_reduce and keep this rank's slice
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
+        c_out = counts[rank * per:(rank + 1) * per].clone()
+        t_out = totals[rank * per:(rank + 1) * per].clone()
+    else:
+        c_out = counts.new_empty((per, NB))
+        t_out = totals.new_empty(per)
+        dist.reduce_scatter_tensor(c_out, counts.contiguous(), op=dist.ReduceOp.SUM, group=group)
+        dist.reduce_scatter_tensor(t_out, totals.contiguous(), op=dist.ReduceOp.SUM, group=group)
+    first = rank * per
+    keep = max(0, min(per, S - first))
+    return c_out[:keep], t_out[:keep], first
