@@ -233,21 +233,35 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds /*
 // Bucket of a non-negative key v < Int.MaxValue, bit-identical to
 // upper_bound(limits, v) (== the Arrays.binarySearch insertion rule of
 // BucketedHistogram.add): a 1664-entry LUT indexed by the exponent and the top
-// 6 mantissa bits of v brackets the bucket from below; each LUT interval
-// contains at most two limits (checked exhaustively on the host when the
-// table is built), so two compares against the LDS limits finish the search.
-__device__ __forceinline__ uint32_t bucket_lut(uint32_t v, const uint16_t* __restrict__ lut,
+// 6 mantissa bits of v brackets the bucket from below (entry bits [10:0]); each
+// LUT interval contains at most two limits (checked exhaustively on the host).
+// For intervals at most 1024 wide (v < 131072) the entry also holds their
+// offsets from the interval start (bits [20:11], [30:21]; 0 = none), so the
+// search is one LDS read and two register compares; wider intervals (offset
+// field 0x3FF) finish with two compares against the LDS-staged limits.
+__device__ __forceinline__ uint32_t bucket_lut(uint32_t v, const uint32_t* __restrict__ lut,
                                                const int32_t* __restrict__ lim) {
-  uint32_t idx;
+  uint32_t idx, start;
   if (v < 64u) {
     idx = v;
+    start = v;
   } else {
-    const int e = 31 - __clz((int)v);
-    idx = 64u + (uint32_t)(e - 6) * 64u + ((v >> (e - 6)) & 63u);
+    const int sh = 25 - __clz((int)v);  // exponent - 6
+    idx = 64u + (uint32_t)sh * 64u + ((v >> sh) & 63u);
+    start = (v >> sh) << sh;
   }
-  uint32_t b = lut[idx];
-  b += (lim[b] <= (int32_t)v) ? 1u : 0u;
-  b += (lim[b] <= (int32_t)v) ? 1u : 0u;
+  const uint32_t x = lut[idx];
+  uint32_t b = x & 0x7FFu;
+  const uint32_t o1 = (x >> 11) & 0x3FFu;
+  const uint32_t o2 = x >> 21;
+  if (o1 == 0x3FFu) {
+    b += (lim[b] <= (int32_t)v) ? 1u : 0u;
+    b += (lim[b] <= (int32_t)v) ? 1u : 0u;
+  } else {
+    const uint32_t d = v - start;
+    b += (o1 != 0u && d >= o1) ? 1u : 0u;
+    b += (o2 != 0u && d >= o2) ? 1u : 0u;
+  }
   return b;
 }
 
@@ -264,7 +278,7 @@ __device__ __forceinline__ uint32_t search_key(int32_t key, const int32_t* __res
 // upstream BucketedHistogram.add(Long) applied to Metric.Stat.add's
 // `value.toLong` (Metric.scala:32): returns the bucket and the sample's
 // contribution to `total` (Int.MaxValue for the overflow bucket).
-__device__ __forceinline__ uint32_t bucketize(float f, const uint16_t* __restrict__ lut,
+__device__ __forceinline__ uint32_t bucketize(float f, const uint32_t* __restrict__ lut,
                                               const int32_t* __restrict__ lim, int64_t& contrib) {
   if (f >= 0.0f && f < 2147483648.0f) {  // common case: v in [0, 2147483520]
     const uint32_t v = (uint32_t)f;
@@ -366,6 +380,25 @@ __device__ __forceinline__ uint32_t hot_rank(uint32_t* ctr, uint32_t key, bool v
   }
   if (!handled) rank = atomicAdd(&ctr[key], 1u);
   return rank;
+}
+
+// ctr[key] += 1 for every valid lane, with the lanes of up to two wave-uniform
+// hot keys merged into one atomic each.  Convergent.
+__device__ __forceinline__ void hot_inc(uint32_t* ctr, uint32_t key, bool valid, uint32_t hot0, uint32_t hot1) {
+  bool handled = !valid;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t hk = h ? hot1 : hot0;
+    if (hk != 0xFFFFFFFFu) {
+      const bool mine = valid && key == hk;
+      const unsigned long long m = __ballot(mine);
+      if (m) {
+        if (lane_id() == __ffsll((long long)m) - 1) atomicAdd(&ctr[hk], (uint32_t)__popcll(m));
+        handled |= mine;
+      }
+    }
+  }
+  if (!handled) atomicAdd(&ctr[key], 1u);
 }
 
 // Visit records r[a, e) with 16-B loads, two in flight per thread per step.

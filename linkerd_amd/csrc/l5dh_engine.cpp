@@ -76,17 +76,31 @@ static int host_bucket(const int32_t* L, int64_t v) {
   return lo;
 }
 
-int build_bucket_lut(const int32_t* L, uint16_t* lut) {
+int build_bucket_lut(const int32_t* L, uint32_t* lut) {
+  // entry = b0 | off1 << 11 | off2 << 21 (offsets of the limits inside the
+  // interval from its start, 0 = none) or off1 = 0x3FF for intervals wider
+  // than 1024 (the device then compares against the limits).
   int maxin = 0, k = 0;
-  for (int v = 0; v < 64; ++v) lut[k++] = (uint16_t)host_bucket(L, v);
+  for (int v = 0; v < 64; ++v) lut[k++] = (uint32_t)host_bucket(L, v);
   for (int e = 6; e <= 30; ++e)
     for (int m = 0; m < 64; ++m) {
       const int64_t start = (int64_t)(64 + m) << (e - 6);
       int64_t end = ((int64_t)(64 + m + 1) << (e - 6)) - 1;
       if (end > 2147483646) end = 2147483646;
       const int b0 = host_bucket(L, start);
-      lut[k++] = (uint16_t)b0;
-      maxin = std::max(maxin, host_bucket(L, end) - b0);
+      const int nin = host_bucket(L, end) - b0;
+      maxin = std::max(maxin, nin);
+      uint32_t x = (uint32_t)b0;
+      if (end - start + 1 <= 1024) {
+        for (int i = 0; i < nin && i < 2; ++i) {
+          const int64_t off = (int64_t)L[b0 + i] - start;  // >= 1: L[b0] > start
+          if (off < 1 || off > 1023) return 99;
+          x |= (uint32_t)off << (11 + 10 * i);
+        }
+      } else {
+        x |= 0x3FFu << 11;
+      }
+      lut[k++] = x;
     }
   return k == LUT_N ? maxin : 99;
 }
@@ -105,7 +119,7 @@ struct l5dh_ctx {
   int32_t* d_lim_pad = nullptr;
   int32_t* d_mid = nullptr;
   int32_t* d_base = nullptr;
-  uint16_t* d_lut = nullptr;
+  uint32_t* d_lut = nullptr;
   // state
   uint32_t* d_counts = nullptr;
   int64_t* d_total = nullptr;
@@ -137,7 +151,7 @@ struct l5dh_ctx {
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
-  uint32_t hot_chunk = 1u << 18;  // records per hot item: the second half-round re-reads them from L2
+  uint32_t hot_chunk = 1u << 18;  // records per big-tile item (u32 LDS bins, one half-tile per workgroup)
   bool timing = false;
   struct Ev {
     int kid;
@@ -283,7 +297,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   Tables tb = tables(c);
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_init(pl, hot, st, c->stream));
+    HIPCHK(c, launch_hot_init(pl, hot, st, c->hot_chunk, c->stream));
   }
   {
     KTimer kt(c, L5DH_K_ACCUM);
@@ -292,7 +306,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   }
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, c->stream));
+    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, c->hot_chunk, c->stream));
   }
   c->nseg = 0;
   return 0;
@@ -347,7 +361,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
   {
     KTimer kt(c, L5DH_K_COUNT);
-    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, vec, c->stream));
+    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + 2040, vec, c->stream));
   }
   {
     KTimer kt(c, L5DH_K_SCAN);
@@ -475,7 +489,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   const size_t S = c->S, F = c->F;
   auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
-            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 2) && mal((void**)&c->d_counts, S * ROW * 4) &&
+            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
             mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
@@ -494,14 +508,15 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
     mid[b] = b == 0 ? 0 : (b >= NL ? INT_MAXV : (int32_t)(((int64_t)hl.L[b - 1] + hl.L[b]) / 2));
     base[b] = b == 0 ? 0 : hl.L[b - 1];
   }
-  uint16_t lut[LUT_N];
+  uint32_t lut[LUT_N];
   if (build_bucket_lut(hl.L, lut) > 2) return bail(-EIO);
   if (hipMemcpy(c->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_lim_pad, lim_pad, sizeof(lim_pad), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
-      hipMemset(c->d_err, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * 2048) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
   *out = c;
   return 0;
@@ -688,7 +703,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->cold_limit = (uint32_t)v;
       return 0;
     case L5DH_PARAM_HOT_CHUNK:
-      if (v < 65536 || v > (1ll << 30)) return fail(c, -EINVAL, "hot chunk must be in [65536, 2^30]");
+      if (v < 1024 || v > (1ll << 30)) return fail(c, -EINVAL, "hot chunk must be in [1024, 2^30]");
       c->hot_chunk = (uint32_t)v;
       return 0;
     case L5DH_PARAM_MAX_SEGMENTS:

@@ -32,18 +32,19 @@ constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by t
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ series, size_t n, size_t per, uint32_t S,
                                               uint32_t F, uint32_t* __restrict__ table, uint32_t* __restrict__ err,
-                                              int vec) {
+                                              const uint32_t* __restrict__ hint, int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* cnt = smem;
   for (uint32_t t = threadIdx.x; t < F; t += WG) cnt[t] = 0;
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
+  const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot tiles of the previous batch (aggregation only)
   bool bad = false;
   auto one = [&](uint32_t s) {
     const bool ok = s < S;
     bad |= !ok;
-    wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
+    hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
   };
   if (lo < hi) {
     size_t done = lo;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
         auto one_in = [&](uint32_t s) {
           const bool ok = in && s < S;
           bad |= in && !ok;
-          wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
+          hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
         };
         one_in(a.x); one_in(a.y); one_in(a.z); one_in(a.w);
       }
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const uint32_t s = i < hi ? series[i] : 0xFFFFFFFFu;
       const bool ok = s < S;
       bad |= i < hi && !ok;
-      wave_atomic_inc<2>(cnt, s >> TILE_SHIFT, ok);
+      hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
     }
   }
   if (bad) atomicOr(err, 1u);
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(1024) void k_tilescan(const uint32_t* __restrict__ 
 }
 
 // Final record of one sample; escapes add their exact sum difference to sumfix.
-__device__ __forceinline__ uint32_t final_record(uint32_t s, float f, const uint16_t* __restrict__ lut,
+__device__ __forceinline__ uint32_t final_record(uint32_t s, float f, const uint32_t* __restrict__ lut,
                                                  const int32_t* __restrict__ lim, int64_t* __restrict__ sumfix) {
   int64_t c;
   const uint32_t b = bucketize(f, lut, lim, c);
@@ -164,8 +165,8 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
                                             int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   int32_t* lim = reinterpret_cast<int32_t*>(smem);
-  uint16_t* lut = reinterpret_cast<uint16_t*>(smem + LIM_PAD);
-  uint32_t* cur = smem + LIM_PAD + LUT_N / 2;
+  uint32_t* lut = smem + LIM_PAD;
+  uint32_t* cur = smem + LIM_PAD + LUT_N;
   for (int i = threadIdx.x; i < LIM_PAD; i += WG) lim[i] = tb.lim_pad[i];
   for (int i = threadIdx.x; i < LUT_N; i += WG) lut[i] = tb.lut[i];
   const uint32_t* row = table + (size_t)blockIdx.x * F;
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
 //                        0xFF = none): tiles holding >= 1/8 of its records
 //   plan[3FS+1], [3FS+2] hot super-tiles: >= 1/8 of all records (or ~0u)
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
+constexpr int HINT_OFF = 2040;  // plan[2040..2041]: hot-tile hints (fixed slot, survives across batches)
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
                                                  uint32_t* __restrict__ plan) {
   __shared__ uint32_t lds[17];
@@ -313,16 +315,19 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   uint32_t nb = 0, gsz = 0, hot = 0xFFFFu;
   uint64_t tot = 0;
+  unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile) of this thread's two biggest tiles
   const uint32_t j = threadIdx.x;
   if (j < FS) {
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;
+    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest tiles of this super-tile
     for (uint32_t t = j * ST_TILES; t < t1; ++t) {
       const uint32_t v = tile_tot[t];
       tot += v;
       if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = t - j * ST_TILES; }
       else if (v > b1) { b1 = v; i1 = t - j * ST_TILES; }
     }
+    tkA = i0 != 0xFF ? (((unsigned long long)b0 << 16) | (j * ST_TILES + i0)) : 0ull;
+    tkB = i1 != 0xFF ? (((unsigned long long)b1 << 16) | (j * ST_TILES + i1)) : 0ull;
     if ((uint64_t)b0 * 8 < tot || b0 == 0) i0 = 0xFF;
     if ((uint64_t)b1 * 8 < tot || b1 == 0) i1 = 0xFF;
     hot = i0 | (i1 << 8);
@@ -358,11 +363,19 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   const unsigned long long key = j < FS ? ((tot << 10) | j) : 0ull;
   const unsigned long long k1 = block_reduce(key, true);
   const unsigned long long k2 = block_reduce(key == k1 ? 0ull : key, true);
+  const unsigned long long t1 = block_reduce(tkA, true);
+  const unsigned long long t2 = block_reduce(tkA == t1 ? tkB : tkA, true);
   if (threadIdx.x == 0) {
     const unsigned long long ks[2] = {k1, k2};
     for (int h = 0; h < 2; ++h) {
       const uint64_t v = ks[h] >> 10;
       plan[3 * FS + 1 + h] = (v > 0 && v * 8 >= grand) ? (uint32_t)(ks[h] & 1023u) : NOKEY;
+    }
+    // hot-tile hints for the next batch's k_count (tiles with >= 1/64 of the records)
+    const unsigned long long ts[2] = {t1, t2};
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t v = ts[h] >> 16;
+      plan[HINT_OFF + h] = (v > 0 && v * 64 >= grand) ? (uint32_t)(ts[h] & 0xFFFFu) : NOKEY;
     }
   }
 }
@@ -377,7 +390,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
                                                 const uint32_t* __restrict__ plan, Tables tb,
                                                 uint32_t* __restrict__ records) {
   __shared__ int32_t lim[LIM_PAD];
-  __shared__ uint16_t lut[LUT_N];
+  __shared__ uint32_t lut[LUT_N];
   __shared__ uint32_t cur[ST_TILES];      // global write position of each tile
   __shared__ uint32_t cnt[ST_TILES];      // records of each tile in this sub-chunk
   __shared__ uint32_t off[ST_TILES];      // their exclusive offsets in stage
@@ -520,8 +533,9 @@ hipError_t set_ingest_attributes() {
 }
 
 hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
-                        uint32_t* table, uint32_t* err, bool vec, hipStream_t st) {
-  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), (size_t)F * 4, st, series, n, per, S, F, table, err, vec ? 1 : 0);
+                        uint32_t* table, uint32_t* err, const uint32_t* hint, bool vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), (size_t)F * 4, st, series, n, per, S, F, table, err, hint,
+                     vec ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -538,7 +552,7 @@ hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
                       int64_t* sumfix, bool vec, hipStream_t st) {
-  const size_t lds = (size_t)LIM_PAD * 4 + LUT_N * 2 + (size_t)F * 4;
+  const size_t lds = (size_t)LIM_PAD * 4 + LUT_N * 4 + (size_t)F * 4;
   hipLaunchKernelGGL(k_bin, dim3(G), dim3(WG), lds, st, series, values, n, per, S, F, table, tile_base, tb, records,
                      sumfix, vec ? 1 : 0);
   return hipGetLastError();

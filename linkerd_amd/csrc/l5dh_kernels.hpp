@@ -32,7 +32,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
   const int32_t* lim_pad;  // [2048] limits padded with Int.MaxValue
   const int32_t* mid;      // [1798] value reported for bucket b
   const int32_t* base;     // [1800] lower limit of bucket b (0 for b == 0), zero padded
-  const uint16_t* lut;     // [LUT_N] lower bound of the bucket of each LUT interval
+  const uint32_t* lut;     // [LUT_N] bucket bracket + in-interval limit offsets (bucket_lut)
 };
 
 struct Segs {              // binned ingest batches awaiting aggregation
@@ -70,8 +70,9 @@ struct Outputs {
 };
 
 // ---- launchers (all enqueue on `st`) ----
+// hint: 2 hot tile ids (or ~0u) used only to merge LDS atomics
 hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
-                        uint32_t* table, uint32_t* err, bool vec, hipStream_t st);
+                        uint32_t* table, uint32_t* err, const uint32_t* hint, bool vec, hipStream_t st);
 hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* tile_tot, hipStream_t st);
 hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_base, hipStream_t st);
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
@@ -90,12 +91,12 @@ hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, co
                        hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
                        hipStream_t st);
-hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st);
+hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
-                             int reset, hipStream_t st);
+                             int reset, uint32_t hot_chunk, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external
 // dense rows ext[count][1798] + ext_total[count].
 hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out,
@@ -104,6 +105,6 @@ hipError_t set_ingest_attributes();
 hipError_t set_snapshot_attributes();
 // LUT for bucket_lut: builds lut[LUT_N] from the limits; returns the largest
 // number of limits inside one LUT interval (the device search assumes <= 2).
-int build_bucket_lut(const int32_t* limits, uint16_t* lut);
+int build_bucket_lut(const int32_t* limits, uint32_t* lut);
 
 }  // namespace l5dh

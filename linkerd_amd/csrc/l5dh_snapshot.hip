@@ -31,7 +31,7 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     plan.tile_tot[t] = tot;
     if (tot > cold_limit) {
       hi += (tot + hot_chunk - 1) / hot_chunk;
-      hot += tot > hot_chunk ? 1u : 0u;
+      hot += 1;
     } else if (final_mode || tot > 0) {
       ci += 1;
     }
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     plan.item_start2[t] = ha;
     if (tot > cold_limit) {
       ha += (tot + hot_chunk - 1) / hot_chunk;
-      if (tot > hot_chunk) plan.hot_list[xa++] = t;
+      plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
       ca += 1;
     }
@@ -64,9 +64,9 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
 
 // k_hot_init: split tiles accumulate with global atomics into state rows, so
 // clean ones start from zero.
-__global__ __launch_bounds__(256) void k_hot_init(const uint32_t* __restrict__ hot_list, State st) {
-  const uint32_t t = hot_list[blockIdx.x];
-  if (st.dirty[t]) return;
+__global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t hot_chunk) {
+  const uint32_t t = plan.hot_list[blockIdx.x];
+  if (st.dirty[t] || plan.tile_tot[t] <= hot_chunk) return;  // single-chunk tiles emit in place
   const uint32_t s0 = t * TILE;
   const uint32_t s1 = min(st.S, s0 + TILE);
   uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
@@ -85,13 +85,13 @@ __device__ __forceinline__ uint32_t find_tile(const uint32_t* __restrict__ item_
   return lo;
 }
 
-struct SrcLds32 {  // u32 row in LDS (warm/hot half-tiles), bins 1798/1799 zero
+struct SrcLds32 {  // u32 row in LDS (half-tiles of big tiles), bins 1798/1799 zero
   const uint32_t* row;
   __device__ __forceinline__ uint4 get4(int b0) const { return *reinterpret_cast<const uint4*>(row + b0); }
 };
 
-// One series of a tile whose new-record counts sit in LDS (`lds`, u16 or u32
-// row) and whose exact offset sum is `offs`: merge with the old state if the
+// One series of a tile whose new-record counts sit in LDS (`lds`, u16-packed or
+// u32 row) and whose exact offset sum is `offs`: merge with the old state if the
 // tile is dirty, write the dense row(s), fold sumfix into the total and, in a
 // final snapshot, emit the HistogramSummary.  One wave.
 template <class SrcL>
@@ -218,76 +218,88 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
 
 }
 
+// Big tiles (> cold_limit records): item = (chunk of <= hot_chunk records, half of
+// the tile's series).  Both halves of a chunk are blocks b and b+8 -- the same XCD
+// under the round-robin dispatch (MI355X_MICROARCH.md), so they stream the chunk
+// together and the second read is served by that XCD's L2 (speed only; results
+// never depend on placement).  A tile with one chunk is finished in place (each
+// half owns its 16 series); chunks of bigger tiles flush with global atomics and
+// k_hot_finish completes them.
 __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                              uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
+                                                  uint32_t cold_limit, uint32_t hot_chunk, int final_mode,
+                                                  int reset) {
+  (void)cold_limit;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t item = blockIdx.x;
   const uint32_t F = st.F;
-  const uint32_t t = find_tile(plan.item_start2, F, item);
-  const uint32_t sub = item - plan.item_start2[t];
+  const uint32_t p = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);  // chunk item
+  const uint32_t half = (blockIdx.x / 8) & 1u;
+  if (p >= plan.item_start2[F]) return;
+  const uint32_t t = find_tile(plan.item_start2, F, p);
+  const uint32_t sub = p - plan.item_start2[t];
   const uint32_t tot = plan.tile_tot[t];
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
-
-  // warm tile or hot chunk: two rounds of 16 series in u32 LDS bins
+  const bool single = tot <= hot_chunk;
   uint32_t* hist = smem;                                                                 // [16][1800]
   unsigned long long* offsum = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16]
-  const bool single = tot <= hot_chunk;
-  const bool dirty = single && st.dirty[t] != 0;
+  {
+    uint4* q = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < 16) offsum[threadIdx.x] = 0;
+  }
+  __syncthreads();
   const uint64_t vlo = (uint64_t)sub * hot_chunk;
   const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
-#pragma unroll 1
-  for (uint32_t half = 0; half < 2; ++half) {
-    {
-      uint4* p = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
-      if (threadIdx.x < 16) offsum[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    for_tile_records(segs, t, vlo, vhi, [&](uint32_t rec) {
-      const uint32_t loc = rec >> 27;
-      if ((loc >> 4) != half) return;
-      const uint32_t l = loc & 15u;
-      const uint32_t b = (rec >> 16) & 0x7FFu;
-      const uint32_t off = rec & 0xFFFFu;
-      atomicAdd(&hist[l * HROW + b], 1u);
-      if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
-    });
-    __syncthreads();
-    const uint32_t s = t * TILE + 16 * half + w;
-    if (s < st.S) {
-      if (single) {
-        emit_series(SrcLds32{hist + w * HROW}, s, offsum[w], dirty, keep, final_mode, st, tb, out);
-      } else {
-        uint32_t* grow = st.counts + (size_t)s * ROW;
-        const uint32_t* hrow = hist + w * HROW;
-        uint64_t bs = 0;
-        for (int b = lane; b < NB; b += 64) {
-          const uint32_t v = hrow[b];
+  for_tile_records(segs, t, vlo, vhi, [&](uint32_t rec) {
+    const uint32_t loc = rec >> 27;
+    if ((loc >> 4) != half) return;
+    const uint32_t l = loc & 15u;
+    const uint32_t b = (rec >> 16) & 0x7FFu;
+    const uint32_t off = rec & 0xFFFFu;
+    atomicAdd(&hist[l * HROW + b], 1u);
+    if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
+  });
+  __syncthreads();
+  const uint32_t s = t * TILE + 16 * half + w;
+  if (s < st.S) {
+    if (single) {
+      emit_series(SrcLds32{hist + w * HROW}, s, offsum[w], st.dirty[t] != 0, keep, final_mode, st, tb, out);
+    } else {
+      uint32_t* grow = st.counts + (size_t)s * ROW;
+      const uint32_t* hrow = hist + w * HROW;
+      uint64_t bs = 0;
+      for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+        const int b = b0 + lane;
+        const uint32_t v = b < NB ? hrow[b] : 0u;
+        if (__ballot(v != 0u)) {
           if (v) {
             bs += (uint64_t)v * (uint64_t)(uint32_t)tb.base[b];
             atomicAdd(&grow[b], v);
           }
         }
-        bs = wave_sum(bs);
-        if (lane == 0) {
-          const uint64_t add = bs + offsum[w];
-          if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
-        }
+      }
+      bs = wave_sum(bs);
+      if (lane == 0) {
+        const uint64_t add = bs + offsum[w];
+        if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
       }
     }
-    __syncthreads();
   }
-  if (single && threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
+  // dirty[t] of a single-chunk tile is updated by k_hot_finish: the other half may
+  // not have read it yet.
 }
 
 // k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
 // write outputs, update state/dirty.
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
-                                                   int reset) {
+                                                   int reset, uint32_t hot_chunk) {
   const uint32_t t = plan.hot_list[blockIdx.x >> 1];
   const uint32_t half = blockIdx.x & 1u;
+  if (plan.tile_tot[t] <= hot_chunk) {  // emitted by k_accum_hot
+    if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
+    return;
+  }
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const uint32_t s = t * TILE + 16 * half + w;
@@ -373,9 +385,9 @@ hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limi
   return hipGetLastError();
 }
 
-hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, hipStream_t st) {
+hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st) {
   if (num_hot == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hot_init, dim3(num_hot), dim3(256), 0, st, plan.hot_list, state);
+  hipLaunchKernelGGL(k_hot_init, dim3(num_hot), dim3(256), 0, st, plan, state, hot_chunk);
   return hipGetLastError();
 }
 
@@ -389,7 +401,8 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
     if (e != hipSuccess) return e;
   }
   if (hot_items) {
-    hipLaunchKernelGGL(k_accum_hot, dim3(hot_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
+    const uint32_t blocks = ((2 * hot_items + 15) / 16) * 16;  // (chunk, half) pairs 8 blocks apart
+    hipLaunchKernelGGL(k_accum_hot, dim3(blocks), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
                        hot_chunk, final_mode, reset);
     return hipGetLastError();
   }
@@ -397,9 +410,10 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
 }
 
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
-                             int reset, hipStream_t st) {
+                             int reset, uint32_t hot_chunk, hipStream_t st) {
   if (num_hot == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hot_finish, dim3(num_hot * 2), dim3(WG), 0, st, plan, state, tb, out, final_mode, reset);
+  hipLaunchKernelGGL(k_hot_finish, dim3(num_hot * 2), dim3(WG), 0, st, plan, state, tb, out, final_mode, reset,
+                     hot_chunk);
   return hipGetLastError();
 }
 

@@ -114,13 +114,14 @@ def test_multi_batch_and_cumulative_snapshots(oracle, reset):
 
 @BIN_MODES
 def test_hot_tile_split_path(oracle, bin_mode):
-    """Warm tiles (cold_limit < records <= hot_chunk: two u32 half-rounds, outputs in
-    place) and hot tiles (> hot_chunk: chunk items + global atomics + k_hot_finish)."""
+    """Big tiles (> cold_limit records): (chunk, half-tile) items with u32 LDS bins;
+    single-chunk tiles emit in place, bigger ones flush with global atomics and are
+    summarized by k_hot_finish."""
     rng = np.random.default_rng(9)
     S = 100
     eng = _engine(S, bin_mode)
     eng.set_param(N.PARAM_COLD_LIMIT, 500)
-    eng.set_param(N.PARAM_HOT_CHUNK, 65536)
+    eng.set_param(N.PARAM_HOT_CHUNK, 20000)
     o = oracle.OracleHistograms(S)
     # series 0..3 (tile 0) hot: 3+ chunks; tiles 1..3 warm; a few cold-ish
     series = np.concatenate([rng.integers(0, 4, 200_000), rng.integers(32, S, 20_000)]).astype(np.uint32)
