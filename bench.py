@@ -87,6 +87,27 @@ def gen_inputs(torch, synth_lib, workload, S, N, rank, stream):
     return series, values
 
 
+# engine timer -> the kernels it brackets (names as in tools/pmc_summary.py)
+PMC_PARTS = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold", "accum_hot"]}
+
+
+def load_pmc_traffic(path, workload, S, N):
+    """HBM bytes per launch from a committed PMC summary (tools/profile_pmc.sh +
+    tools/pmc_summary.py) of the same workload; {} if absent or for another one."""
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    if pm.get("workload") != workload or pm.get("series") != S or pm.get("samples") != N:
+        return {}
+    ks = pm.get("kernels", {})
+    out = {}
+    for name, parts in PMC_PARTS.items():
+        if all(p in ks and "hbm_bytes_per_launch" in ks[p] for p in parts):
+            out[name] = int(sum(ks[p]["hbm_bytes_per_launch"] for p in parts))
+    return out
+
+
 def cpu_baseline(workload, S, N, sample, threads):
     """C oracle (restatement of the JVM Metric.Stat path) on a bounded sample:
     ingest `sample` samples of the same recipe with `threads` workers (per-series
@@ -210,14 +231,11 @@ def main():
         kernels[name] = entry
     dom = max((k for k in kernels if k in KERNEL_ALG_BYTES), key=lambda k: kernels[k]["avg_ms"])
     d = kernels[dom]
-    traffic = None
-    if os.path.exists(args.pmc_json):
-        try:
-            pm = json.load(open(args.pmc_json))
-            if pm.get("workload") == args.workload and pm.get("series") == S and pm.get("samples") == N:
-                traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    pmc = load_pmc_traffic(args.pmc_json, args.workload, S, N)
+    for name, entry in kernels.items():
+        if name in pmc:
+            entry["traffic"] = pmc[name]
+    traffic = pmc.get(dom)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": d["alg_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(d["alg_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "alg_bytes_per_launch": d["alg_bytes"], "avg_launch_ms": d["avg_ms"]}
