@@ -265,6 +265,24 @@ __device__ __forceinline__ uint32_t bucket_lut(uint32_t v, const uint32_t* __res
   return b;
 }
 
+// Exact bucket AND offset from the bucket's lower limit for keys v < 2^21, with one
+// 8-byte LDS read and no limit reads.  Interval = [start, start + 2^sh) of the
+// same (exponent, 6 mantissa bits) as bucket_lut; entry {o1 | o2 << 16, b0 | p << 16}:
+// b0 = bucket(start), o1/o2 = offsets of the (at most two) limits inside the
+// interval (0xFFFF = none), p = start - lower limit of b0.
+__device__ __forceinline__ uint32_t bucket_lut2(uint32_t v, const uint2* __restrict__ lut2, uint32_t& off) {
+  const bool small = v < 64u;
+  const uint32_t sh = small ? 0u : (uint32_t)(25 - __clz((int)v));
+  const uint32_t idx = small ? v : 64u + sh * 64u + ((v >> sh) & 63u);
+  const uint32_t start = (v >> sh) << sh;
+  const uint2 x = lut2[idx];
+  const uint32_t d = v - start;
+  const uint32_t o1 = x.x & 0xFFFFu, o2 = x.x >> 16;
+  const bool k1 = d >= o1, k2 = d >= o2;
+  off = k2 ? d - o2 : (k1 ? d - o1 : d + (x.y >> 16));
+  return (x.y & 0xFFFFu) + (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+}
+
 // Full 11-step search for any int32 key (negative keys come from the Long.toInt
 // wrap of negative samples; rare path).
 __device__ __forceinline__ uint32_t search_key(int32_t key, const int32_t* __restrict__ lim) {

@@ -104,6 +104,46 @@ int build_bucket_lut(const int32_t* L, uint32_t* lut) {
     }
   return k == LUT_N ? maxin : 99;
 }
+
+int build_bucket_lut2(const int32_t* L, uint32_t* lut2) {
+  int k = 0;
+  auto entry = [&](int64_t start, int64_t end) {
+    const int b0 = host_bucket(L, start);
+    uint32_t o[2] = {0xFFFFu, 0xFFFFu};
+    for (int i = 0; i < 2 && b0 + i < NL && L[b0 + i] <= end; ++i) {
+      const int64_t off = (int64_t)L[b0 + i] - start;
+      if (off < 1 || off >= 0xFFFF) return false;
+      o[i] = (uint32_t)off;
+    }
+    if (b0 + 2 < NL && L[b0 + 2] <= end) return false;  // at most two limits per interval
+    const int64_t p = start - (b0 ? (int64_t)L[b0 - 1] : 0);
+    if (p < 0 || p > 0xFFFF) return false;
+    lut2[2 * k] = o[0] | o[1] << 16;
+    lut2[2 * k + 1] = (uint32_t)b0 | (uint32_t)p << 16;
+    ++k;
+    return true;
+  };
+  for (int v = 0; v < 64; ++v)
+    if (!entry(v, v)) return 1;
+  for (int e = 6; e <= 20; ++e)
+    for (int m = 0; m < 64; ++m)
+      if (!entry((int64_t)(64 + m) << (e - 6), ((int64_t)(64 + m + 1) << (e - 6)) - 1)) return 1;
+  if (k != LUT2_N) return 1;
+  // exhaustive check of the device decode (bucket_lut2) against upper_bound
+  for (uint32_t v = 0; v < (1u << 21); ++v) {
+    const uint32_t sh = v < 64 ? 0u : (uint32_t)(25 - __builtin_clz(v));
+    const uint32_t idx = v < 64 ? v : 64u + sh * 64u + ((v >> sh) & 63u);
+    const uint32_t start = (v >> sh) << sh;
+    const uint32_t d = v - start, x0 = lut2[2 * idx], x1 = lut2[2 * idx + 1];
+    const uint32_t o1 = x0 & 0xFFFFu, o2 = x0 >> 16;
+    const bool k1 = d >= o1, k2 = d >= o2;
+    const uint32_t off = k2 ? d - o2 : (k1 ? d - o1 : d + (x1 >> 16));
+    const uint32_t b = (x1 & 0xFFFFu) + k1 + k2;
+    const int hb = host_bucket(L, v);
+    if ((int)b != hb || off != v - (hb ? (uint32_t)L[hb - 1] : 0u)) return 2;
+  }
+  return 0;
+}
 }  // namespace l5dh
 
 struct l5dh_ctx {
@@ -120,6 +160,7 @@ struct l5dh_ctx {
   int32_t* d_mid = nullptr;
   int32_t* d_base = nullptr;
   uint32_t* d_lut = nullptr;
+  uint2* d_lut2 = nullptr;
   // state
   uint32_t* d_counts = nullptr;
   int64_t* d_total = nullptr;
@@ -260,7 +301,7 @@ int ensure(l5dh_ctx* c, DevBuf& b, size_t bytes) {
   return 0;
 }
 
-Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c->d_lut}; }
+Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2}; }
 
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
@@ -489,7 +530,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   const size_t S = c->S, F = c->F;
   auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
-            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_counts, S * ROW * 4) &&
+            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
             mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
@@ -510,7 +551,11 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   }
   uint32_t lut[LUT_N];
   if (build_bucket_lut(hl.L, lut) > 2) return bail(-EIO);
+  static uint32_t lut2[2 * LUT2_N];
+  static int lut2_rc = build_bucket_lut2(hl.L, lut2);  // built and verified once per process
+  if (lut2_rc != 0) return bail(-EIO);
   if (hipMemcpy(c->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_lut2, lut2, sizeof(lut2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_lim_pad, lim_pad, sizeof(lim_pad), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
@@ -531,7 +576,7 @@ int l5dh_close(l5dh_ctx* c) {
     hipEventDestroy(e.b);
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
-  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
+  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
                   c->d_table, c->d_tile_tot, c->d_item_start, c->d_item_start2, c->d_hot_list, c->d_header, c->d_b2plan};
   for (void* p : ptrs)
     if (p) hipFree(p);

@@ -389,13 +389,11 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
                                                 const uint32_t* __restrict__ tile_base,
                                                 const uint32_t* __restrict__ plan, Tables tb,
                                                 uint32_t* __restrict__ records) {
-  __shared__ int32_t lim[LIM_PAD];
-  __shared__ uint32_t lut[LUT_N];
+  __shared__ uint2 lut2[LUT2_N];
   __shared__ uint32_t cur[ST_TILES];      // global write position of each tile
   __shared__ uint32_t cnt[ST_TILES];      // records of each tile in this sub-chunk
   __shared__ uint32_t off[ST_TILES];      // their exclusive offsets in stage
-  __shared__ uint32_t stage[CH2];         // sub-chunk records sorted by tile
-  __shared__ uint8_t stage_tl[CH2];
+  __shared__ uint2 stage[CH2];            // sub-chunk sorted by tile: {record, global index - stage index}
   __shared__ uint32_t seg[2];
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t item = blockIdx.x;
@@ -412,8 +410,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t hp = plan[2 * FS + 1 + j];
   const uint32_t hot0 = (hp & 0xFFu) == 0xFFu ? NOKEY : (hp & 0xFFu);
   const uint32_t hot1 = ((hp >> 8) & 0xFFu) == 0xFFu ? NOKEY : ((hp >> 8) & 0xFFu);
-  for (int i = threadIdx.x; i < LIM_PAD; i += B2_NT) lim[i] = tb.lim_pad[i];
-  for (int i = threadIdx.x; i < LUT_N; i += B2_NT) lut[i] = tb.lut[i];
+  for (int i = threadIdx.x; i < LUT2_N; i += B2_NT) lut2[i] = tb.lut2[i];
   const uint32_t t0 = j * ST_TILES;
   const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
   if (threadIdx.x < 64) {
@@ -468,15 +465,12 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
         const uint32_t tl = r >> 26;
         const uint32_t loc = (r >> 21) & 31u;
         const uint32_t pl = r & 0x1FFFFFu;
-        uint32_t b = 0, o = 0;
-        if (valid) {
-          if (pl < V_ESC) {
-            b = bucket_lut(pl, lut, lim);
-            o = pl - (b ? (uint32_t)lim[b - 1] : 0u);  // bucket width < 2^16 below V_ESC
-          } else {
-            b = pl - V_ESC;
-            o = OFF_ESC;
-          }
+        uint32_t b, o;
+        if (pl < V_ESC) {
+          b = bucket_lut2(pl, lut2, o);
+        } else {
+          b = pl - V_ESC;
+          o = OFF_ESC;
         }
         rec[4 * k + e] = (loc << 27) | (b << 16) | o;
         tlv[4 * k + e] = valid ? tl : 0xFFu;
@@ -484,7 +478,6 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
       }
     }
     __syncthreads();
-    uint32_t total = 0;
     if (threadIdx.x < 64) {  // exclusive scan of the 64 tile counts (one wave)
       const uint32_t v = cnt[threadIdx.x];
       uint32_t x = v;
@@ -499,18 +492,17 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       if (tlv[k] != 0xFFu) {
-        const uint32_t pos = off[tlv[k]] + rank[k];
-        stage[pos] = rec[k];
-        stage_tl[pos] = (uint8_t)tlv[k];
+        const uint32_t o = off[tlv[k]];
+        const uint32_t pos = o + rank[k];
+        stage[pos] = make_uint2(rec[k], cur[tlv[k]] - o);
       }
     }
-    total = off[ST_TILES - 1] + cnt[ST_TILES - 1];
+    const uint32_t total = off[ST_TILES - 1] + cnt[ST_TILES - 1];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += B2_NT) {
-      const uint32_t tl = stage_tl[i];
-      records[cur[tl] + (i - off[tl])] = stage[i];
+      const uint2 e = stage[i];
+      records[e.y + i] = e.x;
     }
-    __syncthreads();
     if (threadIdx.x < 64) {
       cur[threadIdx.x] += cnt[threadIdx.x];
       cnt[threadIdx.x] = 0;

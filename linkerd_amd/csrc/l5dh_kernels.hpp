@@ -27,12 +27,14 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + 16 * 8 + 64;
 
 constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
+constexpr int LUT2_N = 1024;        // exact bucket + offset LUT for keys < 2^21 (64 direct + 15 octaves x 64)
 
 struct Tables {            // constant tables in HBM (a few KB each, L2 resident)
   const int32_t* lim_pad;  // [2048] limits padded with Int.MaxValue
   const int32_t* mid;      // [1798] value reported for bucket b
   const int32_t* base;     // [1800] lower limit of bucket b (0 for b == 0), zero padded
   const uint32_t* lut;     // [LUT_N] bucket bracket + in-interval limit offsets (bucket_lut)
+  const uint2* lut2;       // [LUT2_N] {o1 | o2 << 16, b0 | p << 16} (bucket_lut2)
 };
 
 struct Segs {              // binned ingest batches awaiting aggregation
@@ -106,5 +108,7 @@ hipError_t set_snapshot_attributes();
 // LUT for bucket_lut: builds lut[LUT_N] from the limits; returns the largest
 // number of limits inside one LUT interval (the device search assumes <= 2).
 int build_bucket_lut(const int32_t* limits, uint32_t* lut);
+// LUT for bucket_lut2 (keys < 2^21), verified exhaustively; 0 on success.
+int build_bucket_lut2(const int32_t* limits, uint32_t* lut2);
 
 }  // namespace l5dh
