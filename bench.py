@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--series", type=int, default=None, help="series per rank (default: workload's)")
     p.add_argument("--samples", type=int, default=None, help="samples per rank per step (default: workload's)")
     p.add_argument("--bin-mode", type=int, default=0)
+    p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..512)")
+    p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
     p.add_argument("--cpu-sample", type=int, default=20_000_000, help="samples in the CPU baseline sample (0: skip)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_latest.json"))
@@ -172,6 +174,10 @@ def main():
 
     eng = HistogramEngine(S, device=torch.cuda.current_device())
     eng.set_param(N_.PARAM_BIN_MODE, args.bin_mode)
+    if args.direct_max is not None:
+        eng.set_param(N_.PARAM_DIRECT_MAX, args.direct_max)
+    if args.direct_div is not None:
+        eng.set_param(N_.PARAM_DIRECT_DIV, args.direct_div)
     summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
     counts = torch.empty((S, N_.NBUCKETS), dtype=torch.int32, device=dev)
 
@@ -202,8 +208,9 @@ def main():
 
     # sanity: every sample landed in exactly one bucket of the last snapshot
     got = int(counts.sum(dtype=torch.int64).item())
-    assert got == N, f"bucket counts sum {got} != {N}"
-    assert int(summ[:, 0].sum().item()) == N
+    if not os.environ.get("L5DH_DBG"):  # L5DH_DBG selects timing-only kernel variants
+        assert got == N, f"bucket counts sum {got} != {N}"
+        assert int(summ[:, 0].sum().item()) == N
 
     # per-kernel device time (HIP events on the engine's stream), separate steps
     eng.set_param(N_.PARAM_TIMING, 1)

@@ -265,6 +265,21 @@ __device__ __forceinline__ uint32_t bucket_lut(uint32_t v, const uint32_t* __res
   return b;
 }
 
+// bucket_lut2 split into its LDS read and its decode, so callers can batch the reads.
+__device__ __forceinline__ uint32_t lut2_index(uint32_t v) {
+  const bool small = v < 64u;
+  const uint32_t sh = small ? 0u : (uint32_t)(25 - __clz((int)v));
+  return small ? v : 64u + sh * 64u + ((v >> sh) & 63u);
+}
+__device__ __forceinline__ uint32_t lut2_decode(uint32_t v, uint2 x, uint32_t& off) {
+  const uint32_t sh = v < 64u ? 0u : (uint32_t)(25 - __clz((int)v));
+  const uint32_t d = v - ((v >> sh) << sh);
+  const uint32_t o1 = x.x & 0xFFFFu, o2 = x.x >> 16;
+  const bool k1 = d >= o1, k2 = d >= o2;
+  off = k2 ? d - o2 : (k1 ? d - o1 : d + (x.y >> 16));
+  return (x.y & 0xFFFFu) + (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+}
+
 // Exact bucket AND offset from the bucket's lower limit for keys v < 2^21, with one
 // 8-byte LDS read and no limit reads.  Interval = [start, start + 2^sh) of the
 // same (exponent, 6 mantissa bits) as bucket_lut; entry {o1 | o2 << 16, b0 | p << 16}:
@@ -333,13 +348,13 @@ __device__ __forceinline__ uint32_t wave_atomic_rank(uint32_t* ctr, uint32_t key
   for (int r = 0; r < ROUNDS; ++r) {
     if (!active) break;
     const int leader = __ffsll((long long)active) - 1;
-    const uint32_t lk = __shfl(key, leader, 64);
+    const uint32_t lk = __builtin_amdgcn_readlane(key, leader);
     const bool mine = !done && key == lk;
     const unsigned long long m = __ballot(mine);
     const uint32_t cnt = (uint32_t)__popcll(m);
     uint32_t base = 0;
     if (lane_id() == leader) base = atomicAdd(&ctr[lk], cnt);
-    base = __shfl(base, leader, 64);
+    base = __builtin_amdgcn_readlane(base, leader);
     if (mine) {
       rank = base + mask_below(m);
       done = true;
@@ -359,7 +374,7 @@ __device__ __forceinline__ void wave_atomic_inc(uint32_t* ctr, uint32_t key, boo
   for (int r = 0; r < ROUNDS; ++r) {
     if (!active) break;
     const int leader = __ffsll((long long)active) - 1;
-    const uint32_t lk = __shfl(key, leader, 64);
+    const uint32_t lk = __builtin_amdgcn_readlane(key, leader);
     const bool mine = !done && key == lk;
     const unsigned long long m = __ballot(mine);
     const uint32_t cnt = (uint32_t)__popcll(m);
@@ -388,7 +403,117 @@ __device__ __forceinline__ uint32_t hot_rank(uint32_t* ctr, uint32_t key, bool v
         const int leader = __ffsll((long long)m) - 1;
         uint32_t base = 0;
         if (lane_id() == leader) base = atomicAdd(&ctr[hk], (uint32_t)__popcll(m));
-        base = __shfl(base, leader, 64);
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (mine) {
+          rank = base + mask_below(m);
+          handled = true;
+        }
+      }
+    }
+  }
+  if (!handled) rank = atomicAdd(&ctr[key], 1u);
+  return rank;
+}
+
+// Batched form of hot_rank over a thread's PT keys (~0u = no key): every lane
+// gets the rank atomicAdd(&ctr[key], 1) would give (up to a permutation), but
+// the lanes of the HK wave-uniform hot keys (~0u = unused slot) are counted by
+// ballots over all PT samples first and then take their ranks from ONE LDS
+// atomic per hot key and wave (issued by lanes 0..HK-1 together), so no rank
+// waits on an atomic inside the per-sample loop.  Convergent.
+template <int HK, int PT>
+__device__ __forceinline__ void hot_rank_batch(uint32_t* ctr, const uint32_t (&key)[PT], const uint32_t (&hk)[HK],
+                                               uint32_t (&rank)[PT]) {
+  uint32_t wcnt[HK];
+#pragma unroll
+  for (int h = 0; h < HK; ++h) wcnt[h] = 0;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    bool hot = false;
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      if (hk[h] != 0xFFFFFFFFu) {
+        const bool mine = key[k] == hk[h];
+        wcnt[h] += (uint32_t)__popcll(__ballot(mine));
+        hot |= mine;
+      }
+    }
+    rank[k] = 0;
+    if (!hot && key[k] != 0xFFFFFFFFu) rank[k] = atomicAdd(&ctr[key[k]], 1u);
+  }
+  const int lane = lane_id();
+  uint32_t mycnt = 0, mykey = 0xFFFFFFFFu;
+#pragma unroll
+  for (int h = 0; h < HK; ++h)
+    if (lane == h) {
+      mycnt = wcnt[h];
+      mykey = hk[h];
+    }
+  uint32_t base = 0;
+  if (mycnt != 0 && mykey != 0xFFFFFFFFu) base = atomicAdd(&ctr[mykey], mycnt);
+  uint32_t hb[HK];
+#pragma unroll
+  for (int h = 0; h < HK; ++h) hb[h] = __builtin_amdgcn_readlane(base, h);
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      if (hk[h] != 0xFFFFFFFFu) {
+        const bool mine = key[k] == hk[h];
+        const unsigned long long m = __ballot(mine);
+        if (mine) rank[k] = hb[h] + mask_below(m);
+        hb[h] += (uint32_t)__popcll(m);
+      }
+    }
+  }
+}
+
+// Batched hot_inc: ctr[key[k]] += 1 for every key != ~0u, one LDS atomic per
+// hot key and wave.  Convergent.
+template <int HK, int PT>
+__device__ __forceinline__ void hot_inc_batch(uint32_t* ctr, const uint32_t (&key)[PT], const uint32_t (&hk)[HK]) {
+  uint32_t wcnt[HK];
+#pragma unroll
+  for (int h = 0; h < HK; ++h) wcnt[h] = 0;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    bool hot = false;
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      if (hk[h] != 0xFFFFFFFFu) {
+        const bool mine = key[k] == hk[h];
+        wcnt[h] += (uint32_t)__popcll(__ballot(mine));
+        hot |= mine;
+      }
+    }
+    if (!hot && key[k] != 0xFFFFFFFFu) atomicAdd(&ctr[key[k]], 1u);
+  }
+  const int lane = lane_id();
+  uint32_t mycnt = 0, mykey = 0xFFFFFFFFu;
+#pragma unroll
+  for (int h = 0; h < HK; ++h)
+    if (lane == h) {
+      mycnt = wcnt[h];
+      mykey = hk[h];
+    }
+  if (mycnt != 0 && mykey != 0xFFFFFFFFu) atomicAdd(&ctr[mykey], mycnt);
+}
+
+// hot_rank for HK wave-uniform hot keys (~0u = unused).  Convergent.
+template <int HK>
+__device__ __forceinline__ uint32_t hot_rank_n(uint32_t* ctr, uint32_t key, bool valid, const uint32_t (&hk)[HK]) {
+  uint32_t rank = 0;
+  bool handled = !valid;
+#pragma unroll
+  for (int h = 0; h < HK; ++h) {
+    if (hk[h] != 0xFFFFFFFFu) {
+      const bool mine = valid && key == hk[h];
+      const unsigned long long m = __ballot(mine);
+      if (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&ctr[hk[h]], (uint32_t)__popcll(m));
+        base = __builtin_amdgcn_readlane(base, leader);
         if (mine) {
           rank = base + mask_below(m);
           handled = true;

@@ -14,6 +14,7 @@
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -57,6 +58,8 @@ const HostLimits& host_limits() {
   static HostLimits h;
   return h;
 }
+
+constexpr size_t MAX_BATCH = ((size_t)1 << 30) - 65536;  // samples per binned piece (k_bin1 tags bit 31)
 
 struct DevBuf {
   void* p = nullptr;
@@ -174,7 +177,7 @@ struct l5dh_ctx {
   uint32_t* d_item_start2 = nullptr;
   uint32_t* d_hot_list = nullptr;
   uint32_t* d_header = nullptr;
-  uint32_t* d_b2plan = nullptr;  // level-2 item plan [2*FS+2]
+  uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
   uint32_t* h_header = nullptr;  // pinned
   int G_max = 256;
   // segments
@@ -189,6 +192,9 @@ struct l5dh_ctx {
   // staging
   DevBuf scratch1;  // level-1 records of the two-level partition
   int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level
+  uint32_t direct_max = DIRECT_MAX;  // tiles k_bin1 may write in final form (0: none)
+  int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
+  uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
@@ -371,7 +377,7 @@ int check_err(l5dh_ctx* c) {
 
 int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n) {
   if (n == 0) return 0;
-  if (n > 0xFFFFFFF0ull) return fail(c, -EINVAL, "batch larger than 2^32-16 samples");
+  if (n > MAX_BATCH) return fail(c, -EINVAL, "batch piece larger than 2^30 samples");
   if (c->nseg >= c->max_seg) {
     int r = fold(c);
     if (r) return r;
@@ -402,7 +408,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
   {
     KTimer kt(c, L5DH_K_COUNT);
-    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + 2040, vec, c->stream));
+    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + PLAN_HINT, vec, c->stream));
   }
   {
     KTimer kt(c, L5DH_K_SCAN);
@@ -411,16 +417,19 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   const bool two_level = c->bin_mode != 1;
   if (two_level) {
-    int r = ensure(c, c->scratch1, n * 4 + 16);  // k_bin2 reads whole 16-B groups
+    int r = ensure(c, c->scratch1, (n + BIN1_SCRATCH_PAD) * 4);  // trash bin; k_bin2 reads whole 16-B groups
     if (r) return r;
     {
       KTimer kt(c, L5DH_K_SCAN);
-      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, c->stream));
+      const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
+      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull),
+                              c->direct_max, c->stream));
     }
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
-                            static_cast<uint32_t*>(c->scratch1.p), c->d_sumfix, vec, c->stream));
+                            static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
+                            c->dbg, c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
     HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, tables(c),
@@ -514,6 +523,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   auto* c = new (std::nothrow) l5dh_ctx();
   if (!c) return -ENOMEM;
   c->device = dev;
+  if (const char* d = getenv("L5DH_DBG")) c->dbg = atoi(d);
   c->S = max_series;
   c->F = (max_series + TILE - 1) / TILE;
   auto bail = [&](int code) {
@@ -535,7 +545,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
             mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
-            mal((void**)&c->d_b2plan, 4 * 2048);
+            mal((void**)&c->d_b2plan, 4 * PLAN_WORDS);
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
   if (!ok) {
     (void)hipGetLastError();
@@ -560,7 +570,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
-      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * 2048) != hipSuccess ||
+      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * PLAN_WORDS) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
   *out = c;
@@ -599,7 +609,17 @@ int l5dh_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
   if (n && (!series || !values)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  return do_ingest(c, series, values, n);
+  // batches are binned in pieces below 2^31 samples (k_bin1 tags direct-tile
+  // destinations in bit 31); an id error in one piece is reported after all pieces
+  int rc = 0;
+  for (size_t o = 0; o < n || (n == 0 && o == 0); o += MAX_BATCH) {
+    const size_t m = std::min(n - o, MAX_BATCH);
+    const int r = do_ingest(c, series + o, values + o, m);
+    if (r == -EINVAL && rc == 0 && m) rc = r;
+    else if (r) return r;
+    if (n == 0) break;
+  }
+  return rc;
 }
 
 int l5dh_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {
@@ -763,6 +783,14 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
     case L5DH_PARAM_BIN_MODE:
       if (v < 0 || v > 2) return fail(c, -EINVAL, "bin mode must be 0 (auto), 1 (single) or 2 (two-level)");
       c->bin_mode = (int)v;
+      return 0;
+    case L5DH_PARAM_DIRECT_MAX:
+      if (v < 0 || v > DIRECT_MAX) return fail(c, -EINVAL, "direct tiles must be in [0, 512]");
+      c->direct_max = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_DIRECT_DIV:
+      if (v < 1 || v > 65536) return fail(c, -EINVAL, "direct divisor must be in [1, 65536]");
+      c->direct_div = (uint32_t)v;
       return 0;
     default:
       return fail(c, -EINVAL, "unknown parameter");

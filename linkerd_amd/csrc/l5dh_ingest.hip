@@ -14,6 +14,8 @@
 //   difference went to sumfix[series] (integer atomics, order free).
 // Level-1 record: [31:26] tile in super-tile | [25:21] series in tile |
 //   [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped).
+#include <algorithm>
+
 #include "l5dh_device.hpp"
 
 namespace l5dh {
@@ -21,10 +23,11 @@ namespace {
 
 constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
+constexpr uint32_t NOKEY = 0xFFFFFFFFu;
+constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
 constexpr uint32_t V_ESC = (1u << 21) - 2048u;
 constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
-constexpr int CH1 = 8192;     // samples per level-1 sub-chunk (16 per thread)
-constexpr int FS_MAX = 512;
+constexpr int CH1 = 6144;     // samples per level-1 sub-chunk (12 per thread)
 constexpr int B2_NT = 256;
 constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
 constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
@@ -40,12 +43,8 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
   const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot tiles of the previous batch (aggregation only)
+  const uint32_t hk[2] = {hot0, hot1};
   bool bad = false;
-  auto one = [&](uint32_t s) {
-    const bool ok = s < S;
-    bad |= !ok;
-    hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
-  };
   if (lo < hi) {
     size_t done = lo;
     if (vec) {  // lo and the base pointer are 16-B aligned
@@ -55,10 +54,15 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const size_t wlast = threadIdx.x | 63;  // last lane of this wave: uniform loop bound
       for (; wlast - threadIdx.x + i + 3 * WG < nv; i += 4 * WG) {
         const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
-        one(a.x); one(a.y); one(a.z); one(a.w);
-        one(b.x); one(b.y); one(b.z); one(b.w);
-        one(c.x); one(c.y); one(c.z); one(c.w);
-        one(d.x); one(d.y); one(d.z); one(d.w);
+        const uint32_t sv[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+        uint32_t key[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const bool ok = sv[k] < S;
+          bad |= !ok;
+          key[k] = ok ? sv[k] >> TILE_SHIFT : 0xFFFFFFFFu;
+        }
+        hot_inc_batch<2, 16>(cnt, key, hk);
       }
       for (; i - threadIdx.x < nv; i += WG) {  // convergent: out-of-range lanes pass invalid ids
         uint4 a = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
@@ -197,8 +201,12 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 
 // ------------------------------------------------------------------------
 // Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
-__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
-  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
+// Level-1 payload of a sample outside [0, V_ESC): bucketize, fold the exact sum
+// difference into sumfix, return V_ESC + bucket (or the truncated value when it
+// lands inside the range after all).  Out of line: rare, and 12 inlined copies
+// of the full search would crowd the instruction cache of the hot loop.
+__device__ __attribute__((noinline)) uint32_t payload1_slow(uint32_t s, float f, Tables tb,
+                                                           int64_t* __restrict__ sumfix) {
   int64_t c;
   const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
   if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
@@ -207,144 +215,325 @@ __device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int
   return V_ESC + b;
 }
 
+__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
+  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
+  return payload1_slow(s, f, tb, sumfix);
+}
+
+// Level 1.  Bins = the FS super-tiles (level-1 records of their non-direct
+// tiles, into scratch1) and the ND direct tiles (final records, straight into
+// the final layout), plus a trash bin for sample slots with no sample (batch
+// tail, ids >= S: counted as errors by k_count) written to scratch1[n ..).  Both
+// arrays share the final layout's index space: slab g's records of direct tile t
+// start at tile_base[t] + pre[g][t]; its level-1 records of super-tile j at
+// tile_base[j*64] + sum of pre[g][t] over the non-direct t of j.
+// Per CH1-slot sub-chunk (every slot lands in exactly one bin, so the body has
+// no per-sample branches): one LDS atomic ranks each slot in its bin (the NHOT
+// hottest bins count in lane-private slots: no same-address serialization), a
+// scan gives bin offsets, each slot is staged at its sorted position WITH its
+// destination ({record, dst | direct << 31}), and all CH1 stage entries are
+// written in order.  Batches are < 2^30 samples.
+// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, lut2,
+// direct words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
 __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
-                                                const uint32_t* __restrict__ stplan, uint32_t* __restrict__ out1,
-                                                int64_t* __restrict__ sumfix, int vec) {
+                                                const uint32_t* __restrict__ plan, uint32_t* __restrict__ out1,
+                                                uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
+                                                int vec, int dbg) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t lds9[B1_NT / 64 + 1];
-  uint32_t* stage = smem;                                         // [CH1]
-  uint16_t* stage_st = reinterpret_cast<uint16_t*>(smem + CH1);   // [CH1]
-  uint32_t* stcnt = smem + CH1 + CH1 / 2;                         // [FS_MAX]
-  uint32_t* stoff = stcnt + FS_MAX;
-  uint32_t* stcur = stoff + FS_MAX;
+  uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
+  uint32_t* cnt = smem + 2 * CH1;                                  // [BIN1_BINS]
+  uint2* oc = reinterpret_cast<uint2*>(cnt + BIN1_BINS);           // [BIN1_BINS]
+  uint2* lut2 = oc + BIN1_BINS;                                    // [LUT2_N]
+  uint2* dw = lut2 + LUT2_N;                                       // [1024] {direct bits, direct tiles before}
+  uint8_t* hslot = reinterpret_cast<uint8_t*>(dw + 1024);          // [BIN1_BINS] hot slot of a bin (NHOT: none)
+  uint32_t* hcnt = reinterpret_cast<uint32_t*>(hslot + BIN1_BINS); // [NHOT + 1][64] lane-private hot counters
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t hot0 = stplan[3 * FS + 1], hot1 = stplan[3 * FS + 2];
+  const uint32_t NW = (F + 31) / 32;
+  const uint32_t ND = plan[PLAN_ND];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const uint32_t TB = FS + ND;  // trash bin (NBIN = TB + 1 <= BIN1_BINS)
+  const uint32_t NBIN = TB + 1;
+  const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
   const uint32_t* prow = pre + (size_t)blockIdx.x * F;
+  for (int i = threadIdx.x; i < LUT2_N; i += B1_NT) lut2[i] = tb.lut2[i];
+  for (uint32_t w = threadIdx.x; w < NW; w += B1_NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
+  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += B1_NT) {
+    uint32_t sl = NHOT;
+#pragma unroll
+    for (int q = 0; q < NHOT; ++q)
+      if (plan[3 * FS + 1 + q] == b) sl = (uint32_t)q;
+    hslot[b] = (uint8_t)sl;
+    cnt[b] = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < (NHOT + 1) * 64; i += B1_NT) hcnt[i] = 0;
   for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
     const uint32_t t0 = j * ST_TILES;
     const uint32_t t1 = min(F, t0 + ST_TILES);
     uint32_t acc = tile_base[t0];
-    for (uint32_t t = t0; t < t1; ++t) acc += prow[t];
-    stcur[j] = acc;
-    stcnt[j] = 0;
+    for (uint32_t t = t0; t < t1; ++t)
+      if (!((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) acc += prow[t];
+    oc[j] = make_uint2(0u, acc);
   }
+  for (uint32_t h = threadIdx.x; h < ND; h += B1_NT) {
+    const uint32_t t = plan[PLAN_DLIST + h];
+    oc[FS + h] = make_uint2(0u, (tile_base[t] + prow[t]) | 0x80000000u);
+  }
+  if (threadIdx.x == 0) oc[TB] = make_uint2(0u, trash);
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
-  constexpr int PT = CH1 / B1_NT;  // 16 samples per thread: 4 groups of 4 consecutive
+  constexpr int PT = CH1 / B1_NT;  // slots per thread: PT/4 groups of 4 consecutive
   for (size_t c0 = lo; c0 < hi; c0 += CH1) {
-    uint32_t rec[PT], rank[PT];
-    uint32_t stv[PT];
     uint32_t sv[PT];
     float fv[PT];
+    if (vec && c0 + CH1 <= hi) {
 #pragma unroll
-    for (int k = 0; k < PT / 4; ++k) {
-      const size_t base = c0 + 4 * ((size_t)k * B1_NT + threadIdx.x);
-      if (vec && base + 3 < hi) {
+      for (int k = 0; k < PT / 4; ++k) {
+        const size_t base = c0 + 4 * ((size_t)k * B1_NT + threadIdx.x);
         const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
         const float4 f4 = *reinterpret_cast<const float4*>(values + base);
         sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
         fv[4 * k] = f4.x; fv[4 * k + 1] = f4.y; fv[4 * k + 2] = f4.z; fv[4 * k + 3] = f4.w;
-      } else {
+      }
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool in = base + e < hi;
-          sv[4 * k + e] = in ? series[base + e] : 0xFFFFFFFFu;
-          fv[4 * k + e] = in ? values[base + e] : 0.0f;
-        }
+      for (int k = 0; k < PT; ++k) {
+        const size_t i = c0 + 4 * ((size_t)(k >> 2) * B1_NT + threadIdx.x) + (k & 3);
+        const bool in = i < hi;
+        sv[k] = in ? series[i] : 0xFFFFFFFFu;
+        fv[k] = in ? values[i] : 0.0f;
       }
     }
+    if (dbg & 8) {  // timing: loads only
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < PT; ++k) x ^= sv[k] ^ __float_as_uint(fv[k]);
+      if (x == 0x12345678u) out1[threadIdx.x] = x;
+      continue;
+    }
+    // payloads: the common case inline, samples outside [0, V_ESC) (rare) out of line
+    uint32_t pl[PT];
+    uint32_t escm = 0;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const float f = fv[k];
+      const bool fast = f >= 0.0f && f < (float)V_ESC;
+      pl[k] = fast ? (uint32_t)f : 0u;
+      escm |= (!fast && sv[k] < S) ? (1u << k) : 0u;
+    }
+    if (__ballot(escm != 0u)) {
+#pragma unroll
+      for (int k = 0; k < PT; ++k)
+        if ((escm >> k) & 1u) pl[k] = payload1_slow(sv[k], fv[k], tb, sumfix);
+    }
+    // classify: direct words + bucket LUT (batched LDS reads), then bin and record
+    uint2 dv[PT], lv[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      dv[k] = dw[min(sv[k], S - 1) >> (TILE_SHIFT + 5)];
+      lv[k] = lut2[lut2_index(pl[k])];
+    }
+    uint32_t rec[PT], bn[PT];
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t s = sv[k];
-      stv[k] = 0xFFFFFFFFu;
-      const bool ok = s < S;
-      if (ok) {
-        const uint32_t pl = payload1(s, fv[k], tb, sumfix);
-        rec[k] = (((s >> TILE_SHIFT) & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl;
-        stv[k] = s >> ST_SHIFT;
-      }
-      rank[k] = hot_rank(stcnt, ok ? stv[k] : 0u, ok, hot0, hot1);
+      const uint32_t t = s >> TILE_SHIFT;
+      const uint32_t bit = 1u << (t & 31u);
+      const bool direct = (dv[k].x & bit) != 0u;
+      uint32_t o;
+      const uint32_t b = lut2_decode(pl[k], lv[k], o);
+      const bool esc = pl[k] >= V_ESC;
+      const uint32_t frec = ((s & (TILE - 1)) << 27) | ((esc ? pl[k] - V_ESC : b) << 16) | (esc ? OFF_ESC : o);
+      const uint32_t lrec = ((t & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl[k];
+      rec[k] = direct ? frec : lrec;
+      const uint32_t bin = direct ? FS + dv[k].y + (uint32_t)__popc(dv[k].x & (bit - 1u)) : s >> ST_SHIFT;
+      bn[k] = s < S ? bin : TB;
+    }
+    // ranks: one LDS atomic per slot; hot bins in lane-private counters
+    uint32_t pk[PT];  // [12:0] local rank | [23:13] bin | [27:24] hot slot (NHOT: none)
+#pragma unroll
+    for (int k = 0; k < PT; ++k) pk[k] = hslot[bn[k]];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t sl = pk[k];
+      uint32_t* ctr = sl < (uint32_t)NHOT ? &hcnt[sl * 64 + lane] : &cnt[bn[k]];
+      pk[k] = atomicAdd(ctr, 1u) | (bn[k] << 13) | (sl << 24);
     }
     __syncthreads();
-    uint32_t tot;
+    const uint32_t hkw = wv < NHOT ? plan[3 * FS + 1 + wv] : NOKEY;
+    if (hkw != NOKEY) {  // wave w: lane prefix and total of hot slot w
+      const uint32_t v = hcnt[wv * 64 + lane];
+      uint32_t x = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      hcnt[wv * 64 + lane] = x - v;
+      if (lane == 63) cnt[hkw] = x;
+    }
+    __syncthreads();
     {
-      const uint32_t v = threadIdx.x < FS ? stcnt[threadIdx.x] : 0u;
-      const uint32_t e = block_excl_scan<B1_NT>(v, lds9, &tot);
-      if (threadIdx.x < FS) stoff[threadIdx.x] = e;
+      const uint32_t b0 = 2 * threadIdx.x;
+      const uint32_t v0 = b0 < NBIN ? cnt[b0] : 0u;
+      const uint32_t v1 = b0 + 1 < NBIN ? cnt[b0 + 1] : 0u;
+      const uint32_t e = block_excl_scan<B1_NT>(v0 + v1, lds9, nullptr);
+      if (b0 < NBIN) oc[b0].x = e;
+      if (b0 + 1 < NBIN) oc[b0 + 1].x = e + v0;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      if (stv[k] != 0xFFFFFFFFu) {
-        const uint32_t pos = stoff[stv[k]] + rank[k];
-        stage[pos] = rec[k];
-        stage_st[pos] = (uint16_t)stv[k];
-      }
+      const uint32_t bin = (pk[k] >> 13) & 2047u;
+      const uint32_t r = (pk[k] & 8191u) + hcnt[(pk[k] >> 24) * 64 + lane];  // row NHOT is zero
+      const uint2 x = oc[bin];
+      stage[x.x + r] = make_uint2(rec[k], x.y + r);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < tot; i += B1_NT) {
-      const uint32_t j = stage_st[i];
-      out1[stcur[j] + (i - stoff[j])] = stage[i];
+    for (uint32_t j = threadIdx.x; j < TB; j += B1_NT) {  // cursors advance; the stage carries the destinations
+      oc[j].y += cnt[j];
+      cnt[j] = 0;
     }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
-      stcur[j] += stcnt[j];
-      stcnt[j] = 0;
+    if (threadIdx.x == 0) cnt[TB] = 0;
+    for (uint32_t i = threadIdx.x; i < NHOT * 64; i += B1_NT) hcnt[i] = 0;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
+      const uint2 e = stage[threadIdx.x + k * B1_NT];
+      if (!(dbg & 1)) ((e.y >> 31) ? records : out1)[e.y & 0x7FFFFFFFu] = e.x;
     }
     __syncthreads();
   }
 }
 
-// Super-tile plan (one workgroup, after the tile totals are known):
+// Ingest plan (one workgroup, after the tile totals are known):
 //   plan[0..FS]          level-2 item_start per super-tile (nb_j items of equal
-//                        slab ranges, ~B2_ITEM records each: skew-balanced)
+//                        slab ranges, ~B2_ITEM level-1 records each: skew-balanced;
+//                        0 items for a super-tile whose tiles are all direct/empty)
 //   plan[FS+1 .. 2FS]    slab-range size per super-tile
-//   plan[2FS+1 .. 3FS]   hot tiles of the super-tile (tile-in-ST, byte 0 and 1;
-//                        0xFF = none): tiles holding >= 1/8 of its records
-//   plan[3FS+1], [3FS+2] hot super-tiles: >= 1/8 of all records (or ~0u)
-constexpr uint32_t NOKEY = 0xFFFFFFFFu;
-constexpr int HINT_OFF = 2040;  // plan[2040..2041]: hot-tile hints (fixed slot, survives across batches)
+//   plan[2FS+1 .. 3FS]   hot non-direct tiles of the super-tile (tile-in-ST, byte 0
+//                        and 1; 0xFF = none): >= 1/8 of its level-1 records
+//   plan[3FS+1 .. +NHOT] hot k_bin1 bins (>= 1/64 of all records, or ~0u)
+//   plan[PLAN_DBITS..]   direct tiles (bitmap, word prefixes, list, count)
+//   plan[PLAN_HINT..+1]  hot-tile hints for the next batch's k_count
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
-                                                 uint32_t* __restrict__ plan) {
+                                                 uint32_t* __restrict__ plan, uint32_t thr_min, uint32_t dmax) {
   __shared__ uint32_t lds[17];
   __shared__ unsigned long long best[16];
+  __shared__ uint32_t lhist[33];
+  __shared__ uint32_t sthr;
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu;
-  uint64_t tot = 0;
-  unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile) of this thread's two biggest tiles
   const uint32_t j = threadIdx.x;
+  // direct threshold: smallest power of two (>= thr_min) selecting <= dmax tiles
+  if (j < 33) lhist[j] = 0;
+  __syncthreads();
+  if (dmax > 0)
+    for (uint32_t t = j; t < F; t += 1024) {
+      const uint32_t v = tile_tot[t];
+      if (v >= thr_min && v > 0) atomicAdd(&lhist[31 - __clz((int)v)], 1u);
+    }
+  __syncthreads();
+  if (j == 0) {
+    // cum_k = tiles with v >= thr_min and floor(log2 v) >= k (non-increasing in k):
+    // the smallest k with cum_k <= dmax gives thr = max(thr_min, 2^k)
+    uint32_t thr = NOKEY;
+    if (dmax > 0) {
+      uint32_t cum = 0;
+      int kbest = 32;
+      for (int k = 31; k >= 0; --k) {
+        cum += lhist[k];
+        if (cum > dmax) break;
+        kbest = k;
+      }
+      if (kbest < 32) thr = max(max(thr_min, 1u), 1u << kbest);
+    }
+    sthr = thr;
+  }
+  __syncthreads();
+  const uint32_t thr = sthr;
+  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nd = 0, w0 = 0, w1 = 0;
+  uint64_t ctot = 0, tot = 0;
+  unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile): this thread's two biggest tiles
   if (j < FS) {
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest tiles of this super-tile
+    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest non-direct tiles of this super-tile
+    uint32_t a0 = 0, a1 = 0, k0 = 0xFF, k1 = 0xFF;  // two biggest tiles
     for (uint32_t t = j * ST_TILES; t < t1; ++t) {
       const uint32_t v = tile_tot[t];
+      const uint32_t tl = t - j * ST_TILES;
       tot += v;
-      if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = t - j * ST_TILES; }
-      else if (v > b1) { b1 = v; i1 = t - j * ST_TILES; }
+      if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
+      else if (v > a1) { a1 = v; k1 = tl; }
+      if (v >= thr) {
+        if (tl < 32) w0 |= 1u << tl; else w1 |= 1u << (tl - 32);
+        continue;
+      }
+      ctot += v;
+      if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
+      else if (v > b1) { b1 = v; i1 = tl; }
     }
-    tkA = i0 != 0xFF ? (((unsigned long long)b0 << 16) | (j * ST_TILES + i0)) : 0ull;
-    tkB = i1 != 0xFF ? (((unsigned long long)b1 << 16) | (j * ST_TILES + i1)) : 0ull;
-    if ((uint64_t)b0 * 8 < tot || b0 == 0) i0 = 0xFF;
-    if ((uint64_t)b1 * 8 < tot || b1 == 0) i1 = 0xFF;
+    nd = (uint32_t)(__popc(w0) + __popc(w1));
+    tkA = k0 != 0xFF ? (((unsigned long long)a0 << 16) | (j * ST_TILES + k0)) : 0ull;
+    tkB = k1 != 0xFF ? (((unsigned long long)a1 << 16) | (j * ST_TILES + k1)) : 0ull;
+    if ((uint64_t)b0 * 8 < ctot || b0 == 0) i0 = 0xFF;
+    if ((uint64_t)b1 * 8 < ctot || b1 == 0) i1 = 0xFF;
     hot = i0 | (i1 << 8);
-    uint32_t want = (uint32_t)((tot + B2_ITEM - 1) / B2_ITEM);
-    want = max(1u, min(want, (uint32_t)G));
-    gsz = ((uint32_t)G + want - 1) / want;
-    nb = ((uint32_t)G + gsz - 1) / gsz;
+    if (ctot > 0) {
+      uint32_t want = (uint32_t)((ctot + B2_ITEM - 1) / B2_ITEM);
+      want = max(1u, min(want, (uint32_t)G));
+      gsz = ((uint32_t)G + want - 1) / want;
+      nb = ((uint32_t)G + gsz - 1) / gsz;
+    } else {
+      gsz = (uint32_t)G;
+    }
   }
-  uint32_t total;
+  uint32_t total, ndt;
   const uint32_t e = block_excl_scan<1024>(nb, lds, &total);
+  const uint32_t de = block_excl_scan<1024>(nd, lds, &ndt);
+  // this thread's NHOT biggest k_bin1 bins, descending: (records << 11 | bin)
+  unsigned long long bk[NHOT] = {};
+  auto push = [&](unsigned long long k) {
+#pragma unroll
+    for (int q = 0; q < NHOT; ++q)
+      if (k > bk[q]) {
+        const unsigned long long x = bk[q];
+        bk[q] = k;
+        k = x;
+      }
+  };
   if (j < FS) {
     plan[j] = e;
     plan[FS + 1 + j] = gsz;
     plan[2 * FS + 1 + j] = hot;
+    plan[PLAN_DBITS + 2 * j] = w0;
+    plan[PLAN_DPRE + 2 * j] = de;
+    if (2 * j + 1 < 1024) {
+      plan[PLAN_DBITS + 2 * j + 1] = w1;
+      plan[PLAN_DPRE + 2 * j + 1] = de + (uint32_t)__popc(w0);
+    }
+    uint32_t h = de;
+    for (int q = 0; q < 2; ++q) {
+      uint32_t w = q ? w1 : w0;
+      while (w) {
+        const uint32_t tl = (uint32_t)(__ffs((int)w) - 1) + 32u * q;
+        w &= w - 1u;
+        const uint32_t t = j * ST_TILES + tl;
+        plan[PLAN_DLIST + h] = t;
+        push(((unsigned long long)tile_tot[t] << 11) | (FS + h));
+        ++h;
+      }
+    }
+    if (ctot) push((ctot << 11) | j);
   }
-  if (threadIdx.x == 0) plan[FS] = total;
-  // grand total and the two biggest super-tiles (key = tot << 10 | j), block reductions
+  if (threadIdx.x == 0) {
+    plan[FS] = total;
+    plan[PLAN_ND] = ndt;
+  }
+  // grand total, the two biggest bins and the two biggest tiles (block reductions)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   auto block_reduce = [&](unsigned long long v, bool is_max) -> unsigned long long {
 #pragma unroll
@@ -360,22 +549,30 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     return r;
   };
   const unsigned long long grand = block_reduce(tot, false);
-  const unsigned long long key = j < FS ? ((tot << 10) | j) : 0ull;
-  const unsigned long long k1 = block_reduce(key, true);
-  const unsigned long long k2 = block_reduce(key == k1 ? 0ull : key, true);
+  unsigned long long ks[NHOT];
+  int head = 0;  // this thread's first bin not yet selected
+#pragma unroll
+  for (int q = 0; q < NHOT; ++q) {
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int r = 0; r < NHOT; ++r)
+      if (r == head) mine = bk[r];
+    ks[q] = block_reduce(mine, true);
+    if (mine != 0 && mine == ks[q]) ++head;
+  }
   const unsigned long long t1 = block_reduce(tkA, true);
   const unsigned long long t2 = block_reduce(tkA == t1 ? tkB : tkA, true);
   if (threadIdx.x == 0) {
-    const unsigned long long ks[2] = {k1, k2};
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t v = ks[h] >> 10;
-      plan[3 * FS + 1 + h] = (v > 0 && v * 8 >= grand) ? (uint32_t)(ks[h] & 1023u) : NOKEY;
+    // bins with >= 1/128 of the records: k_bin1 counts them in lane-private slots
+    for (int h = 0; h < NHOT; ++h) {
+      const uint64_t v = ks[h] >> 11;
+      plan[3 * FS + 1 + h] = (v > 0 && v * 128 >= grand) ? (uint32_t)(ks[h] & 2047u) : NOKEY;
     }
     // hot-tile hints for the next batch's k_count (tiles with >= 1/64 of the records)
     const unsigned long long ts[2] = {t1, t2};
     for (int h = 0; h < 2; ++h) {
       const uint64_t v = ts[h] >> 16;
-      plan[HINT_OFF + h] = (v > 0 && v * 64 >= grand) ? (uint32_t)(ts[h] & 0xFFFFu) : NOKEY;
+      plan[PLAN_HINT + h] = (v > 0 && v * 64 >= grand) ? (uint32_t)(ts[h] & 0xFFFFu) : NOKEY;
     }
   }
 }
@@ -410,6 +607,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t hp = plan[2 * FS + 1 + j];
   const uint32_t hot0 = (hp & 0xFFu) == 0xFFu ? NOKEY : (hp & 0xFFu);
   const uint32_t hot1 = ((hp >> 8) & 0xFFu) == 0xFFu ? NOKEY : ((hp >> 8) & 0xFFu);
+  const uint32_t hk[2] = {hot0, hot1};
   for (int i = threadIdx.x; i < LUT2_N; i += B2_NT) lut2[i] = tb.lut2[i];
   const uint32_t t0 = j * ST_TILES;
   const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
@@ -418,9 +616,11 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     uint32_t p0 = 0, p1 = 0;
     if ((uint32_t)lane < nt) {
       const uint32_t t = t0 + lane;
+      const bool direct = (plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u;
       p0 = pre[(size_t)g0 * F + t];
-      p1 = g1 < G ? pre[(size_t)g1 * F + t] : (tile_base[t + 1] - tile_base[t]);
       cur[lane] = tile_base[t] + p0;
+      p1 = g1 < G ? pre[(size_t)g1 * F + t] : (tile_base[t + 1] - tile_base[t]);
+      if (direct) p0 = p1 = 0;  // its records never reach level 1
     }
     cnt[lane] = 0;
 #pragma unroll
@@ -473,10 +673,10 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
           o = OFF_ESC;
         }
         rec[4 * k + e] = (loc << 27) | (b << 16) | o;
-        tlv[4 * k + e] = valid ? tl : 0xFFu;
-        rank[4 * k + e] = hot_rank(cnt, tl, valid, hot0, hot1);
+        tlv[4 * k + e] = valid ? tl : 0xFFFFFFFFu;
       }
     }
+    hot_rank_batch<2, PT>(cnt, tlv, hk, rank);
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of the 64 tile counts (one wave)
       const uint32_t v = cnt[threadIdx.x];
@@ -491,7 +691,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      if (tlv[k] != 0xFFu) {
+      if (tlv[k] != 0xFFFFFFFFu) {
         const uint32_t o = off[tlv[k]];
         const uint32_t pos = o + rank[k];
         stage[pos] = make_uint2(rec[k], cur[tlv[k]] - o);
@@ -499,9 +699,15 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     }
     const uint32_t total = off[ST_TILES - 1] + cnt[ST_TILES - 1];
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < total; i += B2_NT) {
-      const uint2 e = stage[i];
-      records[e.y + i] = e.x;
+    {
+      uint2 ev[PT];
+#pragma unroll
+      for (int k = 0; k < PT; ++k) ev[k] = stage[threadIdx.x + k * B2_NT];
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint32_t i = threadIdx.x + k * B2_NT;
+        if (i < total) records[ev[k].y + i] = ev[k].x;
+      }
     }
     if (threadIdx.x < 64) {
       cur[threadIdx.x] += cnt[threadIdx.x];
@@ -550,16 +756,19 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
   return hipGetLastError();
 }
 
-hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, hipStream_t st) {
-  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, stplan);
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, uint32_t thr_min,
+                         uint32_t dmax, hipStream_t st) {
+  const uint32_t FS = (F + 63) / 64;
+  const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, (uint32_t)BIN1_BINS - 1 - FS);  // + trash bin
+  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, stplan, thr_min, std::min(dmax, cap));
   return hipGetLastError();
 }
 
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       uint32_t* scratch1, int64_t* sumfix, bool vec, hipStream_t st) {
+                       uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
   hipLaunchKernelGGL(k_bin1, dim3(G), dim3(B1_NT), BIN1_LDS, st, series, values, n, per, S, F, pre, tile_base, tb,
-                     stplan, scratch1, sumfix, vec ? 1 : 0);
+                     stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
 

@@ -82,12 +82,26 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
                       int64_t* sumfix, bool vec, hipStream_t st);
 // Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
 // (super-tile -> tiles).  scratch1 holds n level-1 records.
-constexpr size_t BIN1_LDS = (size_t)8192 * 4 + 8192 * 2 + 3 * 512 * 4;
-// Super-tile plan (level-2 items, hot keys); stplan: device scratch of 2048 u32.
-hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, hipStream_t st);
+// Direct tiles: up to DIRECT_MAX tiles with the most records bypass level 2 --
+// k_bin1 writes their final records straight into the final layout.
+constexpr int DIRECT_MAX = 512;
+constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + direct tiles (<= 512)
+constexpr size_t BIN1_LDS = (size_t)6144 * 8 + BIN1_BINS * 12 + LUT2_N * 8 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4;
+constexpr size_t BIN1_SCRATCH_PAD = 6144 + 16;  // scratch1 entries past n (k_bin1 trash bin)
+// Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
+constexpr int PLAN_WORDS = 8192;
+constexpr int PLAN_HINT = 2040;     // [2] hot-tile hints for the next batch's k_count
+constexpr int PLAN_DBITS = 2048;    // [1024] direct-tile bitmap (bit t of word t/32)
+constexpr int PLAN_DPRE = 3072;     // [1024] direct tiles before word w
+constexpr int PLAN_DLIST = 4096;    // [512] direct tile ids, ascending
+constexpr int PLAN_ND = 4608;       // number of direct tiles
+// Super-tile plan (level-2 items, direct tiles, hot keys).  A tile is direct when
+// its records >= max(thr_min, 2^k), k the smallest power keeping <= dmax tiles.
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, uint32_t thr_min,
+                         uint32_t dmax, hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       uint32_t* scratch1, int64_t* sumfix, bool vec, hipStream_t st);
+                       uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st);
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
                        const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
                        hipStream_t st);
