@@ -31,20 +31,31 @@ __device__ __forceinline__ int64_t java_round_nonneg(double x) {
   return (int64_t)fl + (fr >= 0.5 ? 1 : 0);
 }
 
+// DPP lane moves (VALU; no LDS permute): 0x111/0x112/0x114/0x118 = row_shr:1/2/4/8,
+// 0x142 = row_bcast:15 (rows 1, 3), 0x143 = row_bcast:31 (rows 2, 3).  Lanes with no
+// source (or outside the row mask) read 0.  Whole waves only (EXEC all ones).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, ROWS, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, ROWS, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
+  x += dpp64<0x111, 0xF>(x);
+  x += dpp64<0x112, 0xF>(x);
+  x += dpp64<0x114, 0xF>(x);
+  x += dpp64<0x118, 0xF>(x);
+  x += dpp64<0x142, 0xA>(x);
+  x += dpp64<0x143, 0xC>(x);
   return x;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
+__device__ __forceinline__ uint64_t wave_sum(uint64_t x) {  // every lane gets the sum
+  x = wave_incl_scan(x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, 63);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // ---- bin groups ----------------------------------------------------------
@@ -111,7 +122,8 @@ __device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& 
   for (int q = 0; q < 9; ++q) ls += g[q];
   const uint64_t incl = wave_incl_scan(ls);
   const uint64_t excl = incl - ls;
-  const uint64_t num = __shfl(incl, 63, 64);
+  const uint64_t num = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(incl >> 32), 63) << 32) |
+                       __builtin_amdgcn_readlane((uint32_t)incl, 63);
   const double dn = (double)num;
 
   int my_owner = 0;
@@ -271,13 +283,18 @@ __device__ __forceinline__ uint32_t lut2_index(uint32_t v) {
   const uint32_t sh = small ? 0u : (uint32_t)(25 - __clz((int)v));
   return small ? v : 64u + sh * 64u + ((v >> sh) & 63u);
 }
+__device__ __forceinline__ uint32_t sel_u32(bool c, uint32_t a, uint32_t b) {  // branch-free select (v_bfi)
+  const uint32_t m = 0u - (uint32_t)c;
+  return (a & m) | (b & ~m);
+}
 __device__ __forceinline__ uint32_t lut2_decode(uint32_t v, uint2 x, uint32_t& off) {
   const uint32_t sh = v < 64u ? 0u : (uint32_t)(25 - __clz((int)v));
-  const uint32_t d = v - ((v >> sh) << sh);
+  const uint32_t d = v & ((1u << sh) - 1u);  // v - interval start
   const uint32_t o1 = x.x & 0xFFFFu, o2 = x.x >> 16;
   const bool k1 = d >= o1, k2 = d >= o2;
-  off = k2 ? d - o2 : (k1 ? d - o1 : d + (x.y >> 16));
-  return (x.y & 0xFFFFu) + (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+  // off = d - o2 | d - o1 | d + p, without branches
+  off = d - sel_u32(k2, o2, sel_u32(k1, o1, 0u - (x.y >> 16)));
+  return (x.y & 0xFFFFu) + (uint32_t)k1 + (uint32_t)k2;
 }
 
 // Exact bucket AND offset from the bucket's lower limit for keys v < 2^21, with one
@@ -296,6 +313,18 @@ __device__ __forceinline__ uint32_t bucket_lut2(uint32_t v, const uint2* __restr
   const bool k1 = d >= o1, k2 = d >= o2;
   off = k2 ? d - o2 : (k1 ? d - o1 : d + (x.y >> 16));
   return (x.y & 0xFFFFu) + (k1 ? 1u : 0u) + (k2 ? 1u : 0u);
+}
+
+// Bucket of a binned record (l5dh_kernels.hpp) and its contribution to the
+// exact sum: LUT decode of v, or the escaped bucket with contribution 0 (the
+// whole contribution is already in sumfix).
+__device__ __forceinline__ uint32_t record_bucket(uint32_t rec, const uint2* __restrict__ lut2, uint32_t& v) {
+  const uint32_t p = rec & 0x1FFFFFu;
+  uint32_t o;
+  const uint32_t b = lut2_decode(p, lut2[lut2_index(p)], o);
+  const bool esc = p >= V_ESC;
+  v = sel_u32(esc, 0u, p);
+  return sel_u32(esc, p - V_ESC, b);
 }
 
 // Full 11-step search for any int32 key (negative keys come from the Long.toInt

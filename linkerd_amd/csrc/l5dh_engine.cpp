@@ -173,8 +173,8 @@ struct l5dh_ctx {
   // scratch
   uint32_t* d_table = nullptr;  // [G_max][F]
   uint32_t* d_tile_tot = nullptr;
-  uint32_t* d_item_start = nullptr;
-  uint32_t* d_item_start2 = nullptr;
+  uint32_t* d_cold_tile = nullptr;
+  DevBuf hot_item;  // big-tile chunk items (sized per snapshot)
   uint32_t* d_hot_list = nullptr;
   uint32_t* d_header = nullptr;
   uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
@@ -312,7 +312,7 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot, c->d_item_start, c->d_item_start2, c->d_hot_list, c->d_header};
+  return Plan{c->d_tile_tot, c->d_cold_tile, static_cast<uint32_t*>(c->hot_item.p), c->d_hot_list, c->d_header};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -330,6 +330,12 @@ Segs segs_view(l5dh_ctx* c) {
 int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   if (!final_mode && c->nseg == 0) return 0;
   Segs sv = segs_view(c);
+  {
+    size_t recs = 0;
+    for (int j = 0; j < c->nseg; ++j) recs += c->segs[j].n;
+    const int r = ensure(c, c->hot_item, (recs / c->hot_chunk + c->F + 1) * 4);
+    if (r) return r;
+  }
   Plan pl = plan(c);
   {
     KTimer kt(c, L5DH_K_SCAN);
@@ -396,7 +402,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   auto& sg = c->segs[c->nseg];
   {
-    int r = ensure(c, sg.recs, n * 4);
+    int r = ensure(c, sg.recs, n * 4 + 64);  // readers load whole 16-B groups
     if (r) return r;
   }
   // slabs: one workgroup per CU at most, >= 8K samples each, 16-B aligned starts
@@ -535,6 +541,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->num_cu = prop.multiProcessorCount;
   c->G_max = std::max(1, std::min(2 * c->num_cu, 512));
   if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
+  if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   c->stream = c->own_stream;
   const size_t S = c->S, F = c->F;
@@ -543,7 +550,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
-            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_item_start, (F + 1) * 4) && mal((void**)&c->d_item_start2, (F + 1) * 4) &&
+            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
             mal((void**)&c->d_b2plan, 4 * PLAN_WORDS);
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
@@ -587,14 +594,14 @@ int l5dh_close(l5dh_ctx* c) {
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
-                  c->d_table, c->d_tile_tot, c->d_item_start, c->d_item_start2, c->d_hot_list, c->d_header, c->d_b2plan};
+                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
     if (s.tbase) hipFree(s.tbase);
     if (s.recs.p) hipFree(s.recs.p);
   }
-  DevBuf* bufs[] = {&c->scratch1, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
+  DevBuf* bufs[] = {&c->scratch1, &c->hot_item, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
                     &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);

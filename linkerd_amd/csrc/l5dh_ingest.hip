@@ -3,17 +3,14 @@
 //   k_count    LDS tile histogram of each slab of the COO batch -> table[g][t]
 //   k_colscan  per tile, exclusive prefix over slabs (in place) + tile totals
 //   k_tilescan exclusive prefix over tiles -> tile_base[F+1] (final layout)
-//   k_bin1     level 1: slab -> super-tiles (64 tiles), LDS counting sort of
-//              8K-sample sub-chunks, run writes; payload = truncated sample
-//   k_bin2     level 2: (super-tile, slab block) -> per-(slab, tile) segments,
-//              bucket by LUT-bracketed search, final 4-byte records
-//   k_bin      single-level alternative (bucketize + direct scatter)
+//   k_bin1     level 1: slab -> super-tiles (64 tiles) and direct tiles, LDS
+//              counting sort of 6K-sample sub-chunks, run writes
+//   k_bin2     level 2: (super-tile, slab block) -> per-(slab, tile) segments
+//   k_bin      single-level alternative (direct scatter)
 //
-// Final record (u32): [31:27] series in tile | [26:16] bucket | [15:0] off,
-//   off = contribution - base[bucket] when < 0xFFFF, else 0xFFFF and the exact
-//   difference went to sumfix[series] (integer atomics, order free).
-// Level-1 record: [31:26] tile in super-tile | [25:21] series in tile |
-//   [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped).
+// Records (l5dh_kernels.hpp): [31:26] tile in super-tile | [25:21] series in
+//   tile | [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped: the
+//   exact sum difference went to sumfix[series], integer atomics, order free).
 #include <algorithm>
 
 #include "l5dh_device.hpp"
@@ -25,7 +22,6 @@ constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
-constexpr uint32_t V_ESC = (1u << 21) - 2048u;
 constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
 constexpr int CH1 = 6144;     // samples per level-1 sub-chunk (12 per thread)
 constexpr int B2_NT = 256;
@@ -145,34 +141,32 @@ __global__ __launch_bounds__(1024) void k_tilescan(const uint32_t* __restrict__ 
   if (threadIdx.x == 0) tile_base[F] = tot;
 }
 
-// Final record of one sample; escapes add their exact sum difference to sumfix.
-__device__ __forceinline__ uint32_t final_record(uint32_t s, float f, const uint32_t* __restrict__ lut,
-                                                 const int32_t* __restrict__ lim, int64_t* __restrict__ sumfix) {
+// Level-1 payload of a sample outside [0, V_ESC): bucketize, add its exact
+// contribution to sumfix, return V_ESC + bucket (or the truncated value when it
+// lands inside the range after all).  Rare: k_bin1 runs it from a non-unrolled
+// loop so one copy of the full search sits in the hot loop's code.
+__device__ __forceinline__ uint32_t payload1_slow(uint32_t s, float f, Tables tb,
+                                                           int64_t* __restrict__ sumfix) {
   int64_t c;
-  const uint32_t b = bucketize(f, lut, lim, c);
-  const int64_t off = c - (b ? (int64_t)lim[b - 1] : 0);
-  uint32_t o;
-  if ((uint64_t)off < (uint64_t)OFF_ESC) {
-    o = (uint32_t)off;
-  } else {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)off);
-    o = OFF_ESC;
-  }
-  return ((s & (TILE - 1)) << 27) | (b << 16) | o;
+  const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
+  if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
+  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)c);  // whole contribution
+  return V_ESC + b;
 }
 
-// Single-level: bucketize + scatter to the slab's exclusive (slab, tile) segment.
+__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
+  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
+  return payload1_slow(s, f, tb, sumfix);
+}
+
+// Single-level: scatter records to the slab's exclusive (slab, tile) segment.
 __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                             size_t n, size_t per, uint32_t S, uint32_t F,
                                             const uint32_t* __restrict__ table, const uint32_t* __restrict__ tile_base,
                                             Tables tb, uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
                                             int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  int32_t* lim = reinterpret_cast<int32_t*>(smem);
-  uint32_t* lut = smem + LIM_PAD;
-  uint32_t* cur = smem + LIM_PAD + LUT_N;
-  for (int i = threadIdx.x; i < LIM_PAD; i += WG) lim[i] = tb.lim_pad[i];
-  for (int i = threadIdx.x; i < LUT_N; i += WG) lut[i] = tb.lut[i];
+  uint32_t* cur = smem;
   const uint32_t* row = table + (size_t)blockIdx.x * F;
   for (uint32_t t = threadIdx.x; t < F; t += WG) cur[t] = tile_base[t] + row[t];
   __syncthreads();
@@ -181,7 +175,7 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
   if (lo >= hi) return;
   auto one = [&](uint32_t s, float f) {
     if (s >= S) return;
-    const uint32_t rec = final_record(s, f, lut, lim, sumfix);
+    const uint32_t rec = (((s >> TILE_SHIFT) & 63u) << 26) | ((s & (TILE - 1)) << 21) | payload1(s, f, tb, sumfix);
     records[atomicAdd(&cur[s >> TILE_SHIFT], 1u)] = rec;
   };
   size_t done = lo;
@@ -201,28 +195,9 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 
 // ------------------------------------------------------------------------
 // Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
-// Level-1 payload of a sample outside [0, V_ESC): bucketize, fold the exact sum
-// difference into sumfix, return V_ESC + bucket (or the truncated value when it
-// lands inside the range after all).  Out of line: rare, and 12 inlined copies
-// of the full search would crowd the instruction cache of the hot loop.
-__device__ __attribute__((noinline)) uint32_t payload1_slow(uint32_t s, float f, Tables tb,
-                                                           int64_t* __restrict__ sumfix) {
-  int64_t c;
-  const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
-  if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
-  const int64_t off = c - (b ? (int64_t)tb.lim_pad[b - 1] : 0);
-  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)off);
-  return V_ESC + b;
-}
 
-__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
-  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
-  return payload1_slow(s, f, tb, sumfix);
-}
-
-// Level 1.  Bins = the FS super-tiles (level-1 records of their non-direct
-// tiles, into scratch1) and the ND direct tiles (final records, straight into
-// the final layout), plus a trash bin for sample slots with no sample (batch
+// Level 1.  Bins = the FS super-tiles (records of their non-direct tiles, into
+// scratch1) and the ND direct tiles (records straight into the final layout), plus a trash bin for sample slots with no sample (batch
 // tail, ids >= S: counted as errors by k_count) written to scratch1[n ..).  Both
 // arrays share the final layout's index space: slab g's records of direct tile t
 // start at tile_base[t] + pre[g][t]; its level-1 records of super-tile j at
@@ -233,7 +208,7 @@ __device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int
 // scan gives bin offsets, each slot is staged at its sorted position WITH its
 // destination ({record, dst | direct << 31}), and all CH1 stage entries are
 // written in order.  Batches are < 2^30 samples.
-// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, lut2,
+// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31},
 // direct words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
 __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
@@ -247,8 +222,7 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
   uint32_t* cnt = smem + 2 * CH1;                                  // [BIN1_BINS]
   uint2* oc = reinterpret_cast<uint2*>(cnt + BIN1_BINS);           // [BIN1_BINS]
-  uint2* lut2 = oc + BIN1_BINS;                                    // [LUT2_N]
-  uint2* dw = lut2 + LUT2_N;                                       // [1024] {direct bits, direct tiles before}
+  uint2* dw = oc + BIN1_BINS;                                      // [1024] {direct bits, direct tiles before}
   uint8_t* hslot = reinterpret_cast<uint8_t*>(dw + 1024);          // [BIN1_BINS] hot slot of a bin (NHOT: none)
   uint32_t* hcnt = reinterpret_cast<uint32_t*>(hslot + BIN1_BINS); // [NHOT + 1][64] lane-private hot counters
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
@@ -260,7 +234,6 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   const uint32_t NBIN = TB + 1;
   const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
   const uint32_t* prow = pre + (size_t)blockIdx.x * F;
-  for (int i = threadIdx.x; i < LUT2_N; i += B1_NT) lut2[i] = tb.lut2[i];
   for (uint32_t w = threadIdx.x; w < NW; w += B1_NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
   for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += B1_NT) {
     uint32_t sl = NHOT;
@@ -316,53 +289,60 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
       if (x == 0x12345678u) out1[threadIdx.x] = x;
       continue;
     }
-    // payloads: the common case inline, samples outside [0, V_ESC) (rare) out of line
-    uint32_t pl[PT];
-    uint32_t escm = 0;
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const float f = fv[k];
-      const bool fast = f >= 0.0f && f < (float)V_ESC;
-      pl[k] = fast ? (uint32_t)f : 0u;
-      escm |= (!fast && sv[k] < S) ? (1u << k) : 0u;
-    }
-    if (__ballot(escm != 0u)) {
-#pragma unroll
-      for (int k = 0; k < PT; ++k)
-        if ((escm >> k) & 1u) pl[k] = payload1_slow(sv[k], fv[k], tb, sumfix);
-    }
-    // classify: direct words + bucket LUT (batched LDS reads), then bin and record
-    uint2 dv[PT], lv[PT];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      dv[k] = dw[min(sv[k], S - 1) >> (TILE_SHIFT + 5)];
-      lv[k] = lut2[lut2_index(pl[k])];
-    }
-    uint32_t rec[PT], bn[PT];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t s = sv[k];
-      const uint32_t t = s >> TILE_SHIFT;
-      const uint32_t bit = 1u << (t & 31u);
-      const bool direct = (dv[k].x & bit) != 0u;
-      uint32_t o;
-      const uint32_t b = lut2_decode(pl[k], lv[k], o);
-      const bool esc = pl[k] >= V_ESC;
-      const uint32_t frec = ((s & (TILE - 1)) << 27) | ((esc ? pl[k] - V_ESC : b) << 16) | (esc ? OFF_ESC : o);
-      const uint32_t lrec = ((t & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl[k];
-      rec[k] = direct ? frec : lrec;
-      const uint32_t bin = direct ? FS + dv[k].y + (uint32_t)__popc(dv[k].x & (bit - 1u)) : s >> ST_SHIFT;
-      bn[k] = s < S ? bin : TB;
-    }
-    // ranks: one LDS atomic per slot; hot bins in lane-private counters
+    // Per group of 4 slots: payloads (samples outside [0, V_ESC) take a rare
+    // path through this thread's still free stage slots), batched LDS reads of the
+    // direct words, branch-free bin selection, then one rank atomic per slot; hot
+    // bins count in lane-private counters.
+    uint32_t rec[PT];
     uint32_t pk[PT];  // [12:0] local rank | [23:13] bin | [27:24] hot slot (NHOT: none)
 #pragma unroll
-    for (int k = 0; k < PT; ++k) pk[k] = hslot[bn[k]];
+    for (int g = 0; g < PT; g += 4) {
+      uint32_t pl[4];
+      uint32_t escm = 0;
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t sl = pk[k];
-      uint32_t* ctr = sl < (uint32_t)NHOT ? &hcnt[sl * 64 + lane] : &cnt[bn[k]];
-      pk[k] = atomicAdd(ctr, 1u) | (bn[k] << 13) | (sl << 24);
+      for (int q = 0; q < 4; ++q) {
+        const float f = fv[g + q];
+        const bool fast = f >= 0.0f && f < (float)V_ESC;
+        pl[q] = fast ? (uint32_t)f : 0u;
+        escm |= (!fast && sv[g + q] < S) ? (1u << q) : 0u;
+      }
+      if (__ballot(escm != 0u)) {
+        uint32_t* tmp = reinterpret_cast<uint32_t*>(stage) + threadIdx.x * 8;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          tmp[2 * q] = sv[g + q];
+          tmp[2 * q + 1] = __float_as_uint(fv[g + q]);
+        }
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q)
+          if ((escm >> q) & 1u) tmp[2 * q] = payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((escm >> q) & 1u) pl[q] = tmp[2 * q];
+      }
+      uint2 dv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dv[q] = dw[min(sv[g + q], S - 1) >> (TILE_SHIFT + 5)];
+      uint32_t bn[4], sl[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t s = sv[g + q];
+        const uint32_t t = s >> TILE_SHIFT;
+        const uint32_t bit = 1u << (t & 31u);
+        const bool direct = (dv[q].x & bit) != 0u;
+        rec[g + q] = ((t & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl[q];
+        const uint32_t dbin = FS + dv[q].y + (uint32_t)__popc(dv[q].x & (bit - 1u));
+        bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sl[q] = hslot[bn[q]];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool hot = sl[q] < (uint32_t)NHOT;
+        uint32_t* ctr = hot ? hcnt + sl[q] * 64u + (uint32_t)lane : cnt + bn[q];
+        pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 13) | (sl[q] << 24);
+      }
+      asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
     __syncthreads();
     const uint32_t hkw = wv < NHOT ? plan[3 * FS + 1 + wv] : NOKEY;
@@ -586,7 +566,6 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
                                                 const uint32_t* __restrict__ tile_base,
                                                 const uint32_t* __restrict__ plan, Tables tb,
                                                 uint32_t* __restrict__ records) {
-  __shared__ uint2 lut2[LUT2_N];
   __shared__ uint32_t cur[ST_TILES];      // global write position of each tile
   __shared__ uint32_t cnt[ST_TILES];      // records of each tile in this sub-chunk
   __shared__ uint32_t off[ST_TILES];      // their exclusive offsets in stage
@@ -608,7 +587,6 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t hot0 = (hp & 0xFFu) == 0xFFu ? NOKEY : (hp & 0xFFu);
   const uint32_t hot1 = ((hp >> 8) & 0xFFu) == 0xFFu ? NOKEY : ((hp >> 8) & 0xFFu);
   const uint32_t hk[2] = {hot0, hot1};
-  for (int i = threadIdx.x; i < LUT2_N; i += B2_NT) lut2[i] = tb.lut2[i];
   const uint32_t t0 = j * ST_TILES;
   const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
   if (threadIdx.x < 64) {
@@ -663,16 +641,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
         const bool valid = idx >= A && idx < B;
         const uint32_t r = xv[e];
         const uint32_t tl = r >> 26;
-        const uint32_t loc = (r >> 21) & 31u;
-        const uint32_t pl = r & 0x1FFFFFu;
-        uint32_t b, o;
-        if (pl < V_ESC) {
-          b = bucket_lut2(pl, lut2, o);
-        } else {
-          b = pl - V_ESC;
-          o = OFF_ESC;
-        }
-        rec[4 * k + e] = (loc << 27) | (b << 16) | o;
+        rec[4 * k + e] = r;  // records pass through unchanged (tile order is all that changes)
         tlv[4 * k + e] = valid ? tl : 0xFFFFFFFFu;
       }
     }
@@ -750,7 +719,7 @@ hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
                       int64_t* sumfix, bool vec, hipStream_t st) {
-  const size_t lds = (size_t)LIM_PAD * 4 + LUT_N * 4 + (size_t)F * 4;
+  const size_t lds = (size_t)F * 4;
   hipLaunchKernelGGL(k_bin, dim3(G), dim3(WG), lds, st, series, values, n, per, S, F, table, tile_base, tb, records,
                      sumfix, vec ? 1 : 0);
   return hipGetLastError();

@@ -18,13 +18,21 @@ constexpr int TILE_SHIFT = 5;
 constexpr int ROW = 1800;           // state row stride in u32 (16-B aligned rows)
 constexpr int CROW = 900;           // u16-packed cold row in LDS, in u32 words
 constexpr int HROW = 1800;          // u32 hot row in LDS
-constexpr uint32_t OFF_ESC = 0xFFFFu;
+// Binned record (u32), the same at both partition levels and in the final layout:
+//   [31:26] tile in super-tile | [25:21] series in tile | [20:0] payload,
+//   payload = v = (long)sample when 0 <= v < V_ESC, else V_ESC + bucket (the
+//   sample's exact contribution to `total` went to sumfix[series]).
+// The accumulate kernels bucketize v (LUT) and sum the payloads below V_ESC.
+constexpr uint32_t V_ESC = (1u << 21) - 2048u;
 constexpr int MAX_SEG = 8;
 constexpr int WG = 1024;            // threads per workgroup of the heavy kernels
 constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow below this
 
-// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows (hot)
-constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + 16 * 8 + 64;
+// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows
+// (hot), lane-private offset sums, the bucket LUT
+constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8;
+// hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
+constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;
 
 constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
 constexpr int LUT2_N = 1024;        // exact bucket + offset LUT for keys < 2^21 (64 direct + 15 octaves x 64)
@@ -59,8 +67,8 @@ struct State {
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
-  uint32_t* item_start;    // [F+1] cold items (one per cold tile)
-  uint32_t* item_start2;   // [F+1] warm/hot items (one per hot_chunk records)
+  uint32_t* cold_tile;     // [F] cold item -> tile
+  uint32_t* hot_item;      // [hot items] big-tile chunk item -> tile | chunk << 15
   uint32_t* hot_list;      // [F] multi-chunk tiles
   uint32_t* header;        // [4] cold items, multi-chunk tiles, warm/hot items
 };
@@ -86,7 +94,7 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
 // k_bin1 writes their final records straight into the final layout.
 constexpr int DIRECT_MAX = 512;
 constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + direct tiles (<= 512)
-constexpr size_t BIN1_LDS = (size_t)6144 * 8 + BIN1_BINS * 12 + LUT2_N * 8 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4;
+constexpr size_t BIN1_LDS = (size_t)6144 * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4;
 constexpr size_t BIN1_SCRATCH_PAD = 6144 + 16;  // scratch1 entries past n (k_bin1 trash bin)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
 constexpr int PLAN_WORDS = 8192;
@@ -119,6 +127,7 @@ hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total
                        int reset, int64_t* totals_out, hipStream_t st);
 hipError_t set_ingest_attributes();
 hipError_t set_snapshot_attributes();
+hipError_t set_snapshot_debug(int dbg);
 // LUT for bucket_lut: builds lut[LUT_N] from the limits; returns the largest
 // number of limits inside one LUT interval (the device search assumes <= 2).
 int build_bucket_lut(const int32_t* limits, uint32_t* lut);

@@ -13,8 +13,11 @@
 namespace l5dh {
 namespace {
 
+__constant__ int g_dbg;  // L5DH_DBG timing-only variants (results invalid): 0x100 no records, 0x200 no dense stores
+
 // k_plan: one workgroup.  Per tile: records across segments, hot/cold, work
-// items; exclusive scans -> item_start[F+1], hot_list, header {items, hot}.
+// items; exclusive scans -> cold_tile[] (item -> tile), hot_item[] (item -> tile
+// and chunk), hot_list, header {cold items, multi-chunk tiles, hot items}.
 __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
                                                uint32_t hot_chunk, Plan plan) {
   __shared__ uint32_t lds_a[17];
@@ -44,18 +47,16 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     const uint32_t t = t0 + k;
     if (t >= F) break;
     const uint32_t tot = plan.tile_tot[t];
-    plan.item_start[t] = ca;
-    plan.item_start2[t] = ha;
     if (tot > cold_limit) {
-      ha += (tot + hot_chunk - 1) / hot_chunk;
+      const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
+      for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
+      ha += nc;
       plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
-      ca += 1;
+      plan.cold_tile[ca++] = t;
     }
   }
   if (threadIdx.x == 0) {
-    plan.item_start[F] = tot_c;
-    plan.item_start2[F] = tot_h;
     plan.header[0] = tot_c;
     plan.header[1] = tot_hot;
     plan.header[2] = tot_h;
@@ -75,27 +76,17 @@ __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t 
   if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
 }
 
-__device__ __forceinline__ uint32_t find_tile(const uint32_t* __restrict__ item_start, uint32_t F, uint32_t item) {
-  // last t with item_start[t] <= item
-  uint32_t lo = 0, hi = F;  // invariant: item_start[lo] <= item < item_start[hi] (item_start[F] = total)
-  while (hi - lo > 1) {
-    const uint32_t m = (lo + hi) >> 1;
-    if (item_start[m] <= item) lo = m; else hi = m;
-  }
-  return lo;
-}
-
 struct SrcLds32 {  // u32 row in LDS (half-tiles of big tiles), bins 1798/1799 zero
   const uint32_t* row;
   __device__ __forceinline__ uint4 get4(int b0) const { return *reinterpret_cast<const uint4*>(row + b0); }
 };
 
 // One series of a tile whose new-record counts sit in LDS (`lds`, u16-packed or
-// u32 row) and whose exact offset sum is `offs`: merge with the old state if the
+// u32 row) and whose new samples sum to `vsum` (+ sumfix): merge with the old state if the
 // tile is dirty, write the dense row(s), fold sumfix into the total and, in a
 // final snapshot, emit the HistogramSummary.  One wave.
 template <class SrcL>
-__device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_t offs, bool dirty, bool keep,
+__device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_t vsum, bool dirty, bool keep,
                                             int final_mode, State st, Tables tb, Outputs out) {
   const int lane = lane_id();
   const int ng = lane_groups(lane);
@@ -104,7 +95,6 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   int32_t* orow = (emit && out.counts) ? out.counts + (size_t)oi * NB : nullptr;
   uint32_t* srow = st.counts + (size_t)s * ROW;
   uint32_t g[9];
-  uint64_t bs = 0;  // sum_b newcount_b * base_b (+ offs) = exact sum of the new samples
   if (!dirty) {
     // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are padding)
 #pragma unroll 2
@@ -113,8 +103,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
       if (q < NB4) {
         const int b0 = 4 * q;
         const uint4 v = lds.get4(b0);
-        bs += dot4(v, tb.base, b0);
-        if (orow) store4_1798(orow, b0, v);
+        if (orow && !(g_dbg & 0x200)) store4_1798(orow, b0, v);
         if (keep) store4_state(srow, b0, v);
       }
     }
@@ -129,7 +118,6 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
       if (q < ng) {
         const int b0 = 28 * lane + 4 * q;
         const uint4 v = lds.get4(b0);
-        bs += dot4(v, tb.base, b0);
         const uint4 o = old.get4(b0);
         const uint4 cmb = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
         g[q] = sum4(cmb);
@@ -139,8 +127,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
-  bs = wave_sum(bs);
-  int64_t total = (int64_t)(bs + offs) + st.sumfix[s];
+  int64_t total = (int64_t)vsum + st.sumfix[s];
   if (dirty) total += st.total[s];
   if (lane == 0) {
     st.sumfix[s] = 0;
@@ -173,6 +160,48 @@ __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, u
   }
 }
 
+// Records of tile t in the virtual range [vlo, vhi) whose series lies in half
+// `half` (bit 25 = series-in-tile >> 4), visited by full waves: every wave loads
+// 4 records per lane (the next block already in flight), compacts its own-half
+// ones into its LDS queue (ballot + mbcnt), then feeds the queue to fn with all
+// lanes active.
+template <class Fn>
+__device__ __forceinline__ void for_half_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi,
+                                                 uint32_t half, uint32_t* __restrict__ q, Fn&& fn) {
+  const int lane = lane_id();
+  uint64_t vbase = 0;
+  for (int j = 0; j < segs.n; ++j) {
+    const uint32_t a0 = segs.tbase[j][t];
+    const uint32_t e0 = segs.tbase[j][t + 1];
+    const uint64_t len = e0 - a0;
+    const uint64_t lo = vlo > vbase ? vlo : vbase;
+    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+    const uint64_t skip = lo - vbase;
+    vbase += len;
+    if (lo >= hi) continue;
+    const uint32_t a = a0 + (uint32_t)skip;
+    const uint32_t e = a + (uint32_t)(hi - lo);
+    const uint32_t* __restrict__ r = segs.recs[j];
+    const uint32_t a4 = a & ~3u;  // 16-B aligned groups; entries outside [a, e) are masked
+    uint32_t g = a4 + 4u * threadIdx.x;
+    uint4 nx = g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t c = a4; c < e; c += 4u * WG, g += 4u * WG) {
+      const uint32_t x[4] = {nx.x, nx.y, nx.z, nx.w};
+      const uint32_t gn = g + 4u * WG;
+      nx = gn < e ? *reinterpret_cast<const uint4*>(r + gn) : make_uint4(0u, 0u, 0u, 0u);
+      uint32_t nq = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool own = g + k >= a && g + k < e && ((x[k] >> 25) & 1u) == half;
+        const unsigned long long m = __ballot(own);
+        if (own) q[nq + mask_below(m)] = x[k];
+        nq += (uint32_t)__popcll(m);
+      }
+      for (uint32_t i = lane; i < nq; i += 64) fn(q[i]);
+    }
+  }
+}
+
 // k_accum: one work item =
 //   cold tile (<= cold_limit records): 32 series in u16-packed LDS bins, one pass;
 //   warm tile (<= hot_chunk records): two rounds (series 0-15, 16-31) in u32 LDS
@@ -183,27 +212,28 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
                                               uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t item = blockIdx.x;
-  const uint32_t F = st.F;
-  const uint32_t t = find_tile(plan.item_start, F, item);
+  const uint32_t t = plan.cold_tile[item];
   const uint32_t tot = plan.tile_tot[t];
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
 
   {
     uint32_t* hist = smem;                    // [32][900] u16 pairs
-    uint32_t* offsum = smem + TILE * CROW;    // [32]
+    uint32_t* vsl = smem + TILE * CROW;       // [32][64] lane-private value sums (< 1152 x 2^21 per slot)
+    uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);  // [LUT2_N]
+    const int lane = lane_id();
     {
       uint4* p = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < TILE * CROW / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
-      if (threadIdx.x < TILE) offsum[threadIdx.x] = 0;
+      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64) / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
     }
     __syncthreads();
-    for_tile_records(segs, t, 0, tot, [&](uint32_t rec) {
-      const uint32_t loc = rec >> 27;
-      const uint32_t b = (rec >> 16) & 0x7FFu;
-      const uint32_t off = rec & 0xFFFFu;
+    if (!(g_dbg & 0x100)) for_tile_records(segs, t, 0, tot, [&](uint32_t rec) {
+      const uint32_t loc = (rec >> 21) & 31u;
+      uint32_t v;
+      const uint32_t b = record_bucket(rec, lut2, v);
       atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-      if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[loc], off);
+      atomicAdd(&vsl[loc * 64 + lane], v);  // no same-address lanes
     });
     __syncthreads();
     const bool dirty = st.dirty[t] != 0;
@@ -211,7 +241,8 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
       const uint32_t loc = w + 16 * rep;
       const uint32_t s = t * TILE + loc;
       if (s >= st.S) continue;
-      emit_series(SrcLds16{hist + loc * CROW}, s, offsum[loc], dirty, keep, final_mode, st, tb, out);
+      const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
+      emit_series(SrcLds16{hist + loc * CROW}, s, vsum, dirty, keep, final_mode, st, tb, out);
     }
     if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
   }
@@ -230,58 +261,54 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
                                                   int reset) {
   (void)cold_limit;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t F = st.F;
   const uint32_t p = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);  // chunk item
   const uint32_t half = (blockIdx.x / 8) & 1u;
-  if (p >= plan.item_start2[F]) return;
-  const uint32_t t = find_tile(plan.item_start2, F, p);
-  const uint32_t sub = p - plan.item_start2[t];
+  if (p >= plan.header[2]) return;
+  const uint32_t hx = plan.hot_item[p];
+  const uint32_t t = hx & 0x7FFFu;
+  const uint32_t sub = hx >> 15;
   const uint32_t tot = plan.tile_tot[t];
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
   const bool single = tot <= hot_chunk;
-  uint32_t* hist = smem;                                                                 // [16][1800]
-  unsigned long long* offsum = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16]
+  uint32_t* hist = smem;                          // [16][1800]
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] value sums
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + 16 * 64);  // [LUT2_N]
+  uint32_t* wq = reinterpret_cast<uint32_t*>(lut2 + LUT2_N) + w * 256;  // this wave's own-half queue
   {
     uint4* q = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
-    if (threadIdx.x < 16) offsum[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
   }
   __syncthreads();
   const uint64_t vlo = (uint64_t)sub * hot_chunk;
   const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
-  for_tile_records(segs, t, vlo, vhi, [&](uint32_t rec) {
-    const uint32_t loc = rec >> 27;
-    if ((loc >> 4) != half) return;
-    const uint32_t l = loc & 15u;
-    const uint32_t b = (rec >> 16) & 0x7FFu;
-    const uint32_t off = rec & 0xFFFFu;
+  for_half_records(segs, t, vlo, vhi, half, wq, [&](uint32_t rec) {
+    const uint32_t l = (rec >> 21) & 15u;
+    uint32_t v;
+    const uint32_t b = record_bucket(rec, lut2, v);
     atomicAdd(&hist[l * HROW + b], 1u);
-    if (off != 0 && off != OFF_ESC) atomicAdd(&offsum[l], (unsigned long long)off);
+    atomicAdd(&vsl[l * 64 + lane], (unsigned long long)v);  // no same-address lanes
   });
   __syncthreads();
+  const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
   const uint32_t s = t * TILE + 16 * half + w;
   if (s < st.S) {
     if (single) {
-      emit_series(SrcLds32{hist + w * HROW}, s, offsum[w], st.dirty[t] != 0, keep, final_mode, st, tb, out);
+      emit_series(SrcLds32{hist + w * HROW}, s, my_vsum, st.dirty[t] != 0, keep, final_mode, st, tb, out);
     } else {
       uint32_t* grow = st.counts + (size_t)s * ROW;
       const uint32_t* hrow = hist + w * HROW;
-      uint64_t bs = 0;
       for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
         const int b = b0 + lane;
         const uint32_t v = b < NB ? hrow[b] : 0u;
         if (__ballot(v != 0u)) {
-          if (v) {
-            bs += (uint64_t)v * (uint64_t)(uint32_t)tb.base[b];
-            atomicAdd(&grow[b], v);
-          }
+          if (v) atomicAdd(&grow[b], v);
         }
       }
-      bs = wave_sum(bs);
       if (lane == 0) {
-        const uint64_t add = bs + offsum[w];
+        const uint64_t add = my_vsum;
         if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
       }
     }
@@ -373,10 +400,12 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
 
 }  // namespace
 
+hipError_t set_snapshot_debug(int dbg) { return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dbg, sizeof(int)); }
+
 hipError_t set_snapshot_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
@@ -402,7 +431,7 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
   }
   if (hot_items) {
     const uint32_t blocks = ((2 * hot_items + 15) / 16) * 16;  // (chunk, half) pairs 8 blocks apart
-    hipLaunchKernelGGL(k_accum_hot, dim3(blocks), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
+    hipLaunchKernelGGL(k_accum_hot, dim3(blocks), dim3(WG), ACC_HOT_LDS, st, segs, plan, state, tb, out, cold_limit,
                        hot_chunk, final_mode, reset);
     return hipGetLastError();
   }

@@ -40,21 +40,30 @@ __global__ __launch_bounds__(NT) void kl(uint32_t* out, uint32_t span, uint32_t 
   uint32_t acc = 0;
   uint32_t h = hsh(threadIdx.x * 7919u + blockIdx.x * 104729u + seed);
   const uint32_t lane = threadIdx.x & 63;
-#pragma unroll 16
-  for (int it = 0; it < ITER; ++it) {
+  uint32_t ad[16];  // addresses precomputed: the loop is LDS-only
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
     uint32_t a;
-    if (PAT == 0) a = (threadIdx.x + it * 64u) & (span - 1);
+    if (PAT == 0) a = (threadIdx.x + k * 64u) & (span - 1);
     else if (PAT == 1) a = h & (span - 1);
-    else if (PAT == 2) a = ((threadIdx.x >> 6) * 97u + it) & (span - 1);
+    else if (PAT == 2) a = ((threadIdx.x >> 6) * 97u + k) & (span - 1);
     else a = h & 31u;
-    h = h * 1664525u + 1013904223u;  // cheap LCG step
+    h = h * 1664525u + 1013904223u;
     h ^= h >> 13;
-    if (OP == 0) atomicAdd(&lds[a], 1u);
-    else if (OP == 1) acc += atomicAdd(&lds[a], 1u);
-    else if (OP == 2) lds[a] = it;
-    else if (OP == 3) acc += lds[a];
-    else if (OP == 4) atomicAdd(reinterpret_cast<unsigned long long*>(&lds[a & ~1u]), 1ull);
-    else if (OP == 5) h += atomicAdd(&lds[a], 1u);
+    ad[k] = a;
+  }
+  for (int it = 0; it < ITER / 16; ++it) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t a = ad[k];
+      if (OP == 0) atomicAdd(&lds[a], 1u);
+      else if (OP == 1) acc += atomicAdd(&lds[a], 1u);
+      else if (OP == 2) lds[a] = it;
+      else if (OP == 3) acc += lds[a];
+      else if (OP == 4) atomicAdd(reinterpret_cast<unsigned long long*>(&lds[a & ~1u]), 1ull);
+      else if (OP == 5) acc += atomicAdd(&lds[a], 1u);
+    }
+    asm volatile("" ::: "memory");
   }
   (void)lane;
   __syncthreads();
