@@ -142,6 +142,27 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   }
 }
 
+// Count a batch of K records per lane (~0u: no record): all bucket-LUT reads are
+// issued before any LDS atomic (the compiler cannot move a read above an atomic
+// it may alias), then per record one histogram atomic and one lane-private sum.
+template <int K, class Hist, class Sum>
+__device__ __forceinline__ void count_batch(const uint32_t (&rec)[K], const uint2* __restrict__ lut2, Hist&& hist_add,
+                                            Sum&& sum_add) {
+  uint2 lv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) lv[k] = lut2[lut2_index(rec[k] & 0x1FFFFFu)];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (rec[k] == 0xFFFFFFFFu) continue;
+    const uint32_t p = rec[k] & 0x1FFFFFu;
+    uint32_t o;
+    const uint32_t b = lut2_decode(p, lv[k], o);
+    const bool esc = p >= V_ESC;
+    hist_add((rec[k] >> 21) & 31u, sel_u32(esc, p - V_ESC, b));
+    sum_add((rec[k] >> 21) & 31u, sel_u32(esc, 0u, p));
+  }
+}
+
 // Records of tile t in the virtual range [vlo, vhi) of its concatenated segments.
 template <class Fn>
 __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi, Fn&& fn) {
@@ -161,10 +182,10 @@ __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, u
 }
 
 // Records of tile t in the virtual range [vlo, vhi) whose series lies in half
-// `half` (bit 25 = series-in-tile >> 4), visited by full waves: every wave loads
-// 4 records per lane (the next block already in flight), compacts its own-half
-// ones into its LDS queue (ballot + mbcnt), then feeds the queue to fn with all
-// lanes active.
+// `half` (bit 25 = series-in-tile >> 4), visited by full waves: every lane loads
+// 8 records per block (the next block already in flight: 32 B per lane), the
+// wave compacts its own-half ones, 4 at a time, into its LDS queue (ballot +
+// mbcnt) and hands the queue to fn as one batch of 4 entries per lane (~0u: none).
 template <class Fn>
 __device__ __forceinline__ void for_half_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi,
                                                  uint32_t half, uint32_t* __restrict__ q, Fn&& fn) {
@@ -183,21 +204,36 @@ __device__ __forceinline__ void for_half_records(const Segs& segs, uint32_t t, u
     const uint32_t e = a + (uint32_t)(hi - lo);
     const uint32_t* __restrict__ r = segs.recs[j];
     const uint32_t a4 = a & ~3u;  // 16-B aligned groups; entries outside [a, e) are masked
+    auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
     uint32_t g = a4 + 4u * threadIdx.x;
-    uint4 nx = g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t c = a4; c < e; c += 4u * WG, g += 4u * WG) {
-      const uint32_t x[4] = {nx.x, nx.y, nx.z, nx.w};
-      const uint32_t gn = g + 4u * WG;
-      nx = gn < e ? *reinterpret_cast<const uint4*>(r + gn) : make_uint4(0u, 0u, 0u, 0u);
-      uint32_t nq = 0;
+    uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
+    for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
+      const uint4 x0 = n0, x1 = n1;
+      n0 = ld(g + 8u * WG);
+      n1 = ld(g + 12u * WG);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool own = g + k >= a && g + k < e && ((x[k] >> 25) & 1u) == half;
-        const unsigned long long m = __ballot(own);
-        if (own) q[nq + mask_below(m)] = x[k];
-        nq += (uint32_t)__popcll(m);
+      for (int h = 0; h < 2; ++h) {
+        const uint4 xx = h ? x1 : x0;
+        const uint32_t gh = g + h * 4u * WG;
+        const uint32_t x[4] = {xx.x, xx.y, xx.z, xx.w};
+        uint32_t nq = 0;
+        if (g_dbg & 0x800) {  // timing: loads only
+          if ((x[0] ^ x[1] ^ x[2] ^ x[3]) == 0x12345u) q[lane] = x[0];
+          continue;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool own = gh + k >= a && gh + k < e && ((x[k] >> 25) & 1u) == half;
+          const unsigned long long m = __ballot(own);
+          if (own) q[nq + mask_below(m)] = x[k];
+          nq += (uint32_t)__popcll(m);
+        }
+        if (g_dbg & 0x400) continue;  // timing: no counting
+        uint32_t rv[4];  // nq <= 256: at most 4 entries per lane, handed over as one batch
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rv[k] = lane + 64u * k < nq ? q[lane + 64 * k] : 0xFFFFFFFFu;
+        fn(rv);
       }
-      for (uint32_t i = lane; i < nq; i += 64) fn(q[i]);
     }
   }
 }
@@ -222,19 +258,51 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
     uint32_t* vsl = smem + TILE * CROW;       // [32][64] lane-private value sums (< 1152 x 2^21 per slot)
     uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);  // [LUT2_N]
     const int lane = lane_id();
+    auto count = [&](uint32_t rec) {
+      const uint32_t loc = (rec >> 21) & 31u;
+      uint32_t v;
+      const uint32_t b = record_bucket(rec, lut2, v);
+      atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+      atomicAdd(&vsl[loc * 64 + lane], v);  // no same-address lanes
+    };
+    // one pending segment (the common case): the tile's first 8 records per lane
+    // are loaded before the LDS is cleared, so their latency overlaps the clearing
+    const bool one = segs.n == 1 && !(g_dbg & 0x100);
+    const uint32_t a = one ? segs.tbase[0][t] : 0u, e = one ? segs.tbase[0][t + 1] : 0u;  // no segment: no read
+    const uint32_t a4 = a & ~3u;
+    auto ld = [&](uint32_t g) {
+      return g < e ? *reinterpret_cast<const uint4*>(segs.recs[0] + g) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint32_t g = a4 + 4u * threadIdx.x;
+    uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+    if (one) {
+      n0 = ld(g);
+      n1 = ld(g + 4u * WG);
+    }
     {
       uint4* p = reinterpret_cast<uint4*>(smem);
       for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64) / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
       for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
     }
     __syncthreads();
-    if (!(g_dbg & 0x100)) for_tile_records(segs, t, 0, tot, [&](uint32_t rec) {
-      const uint32_t loc = (rec >> 21) & 31u;
-      uint32_t v;
-      const uint32_t b = record_bucket(rec, lut2, v);
-      atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-      atomicAdd(&vsl[loc * 64 + lane], v);  // no same-address lanes
-    });
+    if (one) {
+      for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
+        const uint4 x0 = n0, x1 = n1;
+        n0 = ld(g + 8u * WG);
+        n1 = ld(g + 12u * WG);
+        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+        }
+        count_batch<8>(
+            x, lut2, [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u); },
+            [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[loc * 64 + lane], v); });
+      }
+    } else if (!(g_dbg & 0x100)) {
+      for_tile_records(segs, t, 0, tot, count);
+    }
     __syncthreads();
     const bool dirty = st.dirty[t] != 0;
     for (int rep = 0; rep < 2; ++rep) {
@@ -284,12 +352,10 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   __syncthreads();
   const uint64_t vlo = (uint64_t)sub * hot_chunk;
   const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
-  for_half_records(segs, t, vlo, vhi, half, wq, [&](uint32_t rec) {
-    const uint32_t l = (rec >> 21) & 15u;
-    uint32_t v;
-    const uint32_t b = record_bucket(rec, lut2, v);
-    atomicAdd(&hist[l * HROW + b], 1u);
-    atomicAdd(&vsl[l * 64 + lane], (unsigned long long)v);  // no same-address lanes
+  for_half_records(segs, t, vlo, vhi, half, wq, [&](const uint32_t (&rv)[4]) {
+    count_batch<4>(
+        rv, lut2, [&](uint32_t loc, uint32_t b) { if (!(g_dbg & 0x2000)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
+        [&](uint32_t loc, uint32_t v) { if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
   });
   __syncthreads();
   const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
@@ -300,7 +366,7 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
     } else {
       uint32_t* grow = st.counts + (size_t)s * ROW;
       const uint32_t* hrow = hist + w * HROW;
-      for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+      for (int b0 = 0; b0 < ((g_dbg & 0x1000) ? 0 : NB); b0 += 64) {  // 64 consecutive bins per wave atomic
         const int b = b0 + lane;
         const uint32_t v = b < NB ? hrow[b] : 0u;
         if (__ballot(v != 0u)) {
