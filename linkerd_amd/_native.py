@@ -15,7 +15,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libl5dhist.so")
+# L5DH_LIB selects another build of the same library (A/B timing of kernel variants: tools/ab.sh)
+LIB_PATH = os.environ.get("L5DH_LIB") or os.path.join(PKG_DIR, "lib", "libl5dhist.so")
 SYNTH_PATH = os.path.join(PKG_DIR, "lib", "libl5dsynth.so")
 HEADER_PATH = os.path.join(REPO_DIR, "include", "l5dhist.h")
 

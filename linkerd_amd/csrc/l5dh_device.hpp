@@ -41,6 +41,16 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   x += dpp64<0x111, 0xF>(x);
   x += dpp64<0x112, 0xF>(x);

@@ -23,7 +23,6 @@ constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
 constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
-constexpr int CH1 = 6144;     // samples per level-1 sub-chunk (12 per thread)
 constexpr int B2_NT = 256;
 constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
 constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
@@ -208,9 +207,10 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 // scan gives bin offsets, each slot is staged at its sorted position WITH its
 // destination ({record, dst | direct << 31}), and all CH1 stage entries are
 // written in order.  Batches are < 2^30 samples.
-// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31},
-// direct words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
-__global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, direct
+// words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
+template <int CH1, int WPS>
+__global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
@@ -218,10 +218,9 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
                                                 uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
                                                 int vec, int dbg) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  __shared__ uint32_t lds9[B1_NT / 64 + 1];
   uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
   uint32_t* cnt = smem + 2 * CH1;                                  // [BIN1_BINS]
-  uint2* oc = reinterpret_cast<uint2*>(cnt + BIN1_BINS);           // [BIN1_BINS]
+  uint2* oc = reinterpret_cast<uint2*>(cnt + BIN1_BINS);           // [BIN1_BINS] {stage offset, cursor | direct << 31}
   uint2* dw = oc + BIN1_BINS;                                      // [1024] {direct bits, direct tiles before}
   uint8_t* hslot = reinterpret_cast<uint8_t*>(dw + 1024);          // [BIN1_BINS] hot slot of a bin (NHOT: none)
   uint32_t* hcnt = reinterpret_cast<uint32_t*>(hslot + BIN1_BINS); // [NHOT + 1][64] lane-private hot counters
@@ -230,8 +229,7 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
   const uint32_t ND = plan[PLAN_ND];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const uint32_t TB = FS + ND;  // trash bin (NBIN = TB + 1 <= BIN1_BINS)
-  const uint32_t NBIN = TB + 1;
+  const uint32_t TB = FS + ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
   const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
   const uint32_t* prow = pre + (size_t)blockIdx.x * F;
   for (uint32_t w = threadIdx.x; w < NW; w += B1_NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
@@ -345,26 +343,32 @@ __global__ __launch_bounds__(B1_NT, 4) void k_bin1(const uint32_t* __restrict__ 
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
     __syncthreads();
-    const uint32_t hkw = wv < NHOT ? plan[3 * FS + 1 + wv] : NOKEY;
-    if (hkw != NOKEY) {  // wave w: lane prefix and total of hot slot w
-      const uint32_t v = hcnt[wv * 64 + lane];
-      uint32_t x = v;
+    if (wv == 0) {  // one wave: hot-slot lane prefixes and totals, then the bin scan (DPP, no barriers)
+      uint32_t hv[NHOT];
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
+      for (int h = 0; h < NHOT; ++h) hv[h] = hcnt[h * 64 + lane];  // rows of unused slots are zero
+#pragma unroll
+      for (int h = 0; h < NHOT; ++h) {
+        const uint32_t x = wave_incl_scan32(hv[h]);
+        hcnt[h * 64 + lane] = x - hv[h];
+        const uint32_t hk = plan[3 * FS + 1 + h];
+        if (lane == 63 && hk != NOKEY) cnt[hk] = x;
       }
-      hcnt[wv * 64 + lane] = x - v;
-      if (lane == 63) cnt[hkw] = x;
-    }
-    __syncthreads();
-    {
-      const uint32_t b0 = 2 * threadIdx.x;
-      const uint32_t v0 = b0 < NBIN ? cnt[b0] : 0u;
-      const uint32_t v1 = b0 + 1 < NBIN ? cnt[b0 + 1] : 0u;
-      const uint32_t e = block_excl_scan<B1_NT>(v0 + v1, lds9, nullptr);
-      if (b0 < NBIN) oc[b0].x = e;
-      if (b0 + 1 < NBIN) oc[b0 + 1].x = e + v0;
+      uint32_t c[16];  // lane l scans bins [16 l, 16 l + 16)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cnt + 16 * lane + 4 * q);
+        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+      }
+      uint32_t tl = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tl += c[q];
+      uint32_t e = wave_incl_scan32(tl) - tl;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        oc[16 * lane + q].x = e;
+        e += c[q];
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -694,8 +698,10 @@ hipError_t set_ingest_attributes() {
   const int big = 160 * 1024;
   if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BIN1_LDS)))
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bin1_lds(6144))))
     return e;
+
   return hipSuccess;
 }
 
@@ -736,8 +742,8 @@ hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* 
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
                        uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
-  hipLaunchKernelGGL(k_bin1, dim3(G), dim3(B1_NT), BIN1_LDS, st, series, values, n, per, S, F, pre, tile_base, tb,
-                     stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+  hipLaunchKernelGGL((k_bin1<6144, 4>), dim3(G), dim3(B1_NT), bin1_lds(6144), st, series, values, n, per, S, F, pre,
+                     tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
 
