@@ -136,25 +136,24 @@ __device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& 
                        __builtin_amdgcn_readlane((uint32_t)incl, 63);
   const double dn = (double)num;
 
+  // lane k < 8 computes target k (min, p50, p90, p95, p99, p999, p9999, max) in
+  // parallel; each target's owner lane is then found with one ballot
+  uint64_t my_t;
+  {
+    const double p = lane == 1 ? 0.50 : lane == 2 ? 0.90 : lane == 3 ? 0.95 : lane == 4 ? 0.99
+                   : lane == 5 ? 0.999 : 0.9999;
+    my_t = (uint64_t)java_round_nonneg(__dmul_rn(p, dn));
+    if (lane == 0) my_t = num ? 1 : 0;
+    if (lane >= 7) my_t = num;
+  }
   int my_owner = 0;
-  uint64_t my_t = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    uint64_t t;
-    if (k == 0)
-      t = num ? 1 : 0;
-    else if (k == 7)
-      t = num;
-    else {
-      const double p = k == 1 ? 0.50 : k == 2 ? 0.90 : k == 3 ? 0.95 : k == 4 ? 0.99 : k == 5 ? 0.999 : 0.9999;
-      t = (uint64_t)java_round_nonneg(__dmul_rn(p, dn));
-    }
+    const uint64_t t = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_t >> 32), k) << 32) |
+                       __builtin_amdgcn_readlane((uint32_t)my_t, k);
     const unsigned long long m = __ballot(t != 0 && excl < t && t <= incl);
     const int owner = m ? (__ffsll((long long)m) - 1) : 0;
-    if (lane == k) {
-      my_owner = owner;
-      my_t = t;
-    }
+    if (lane == k) my_owner = owner;
   }
   uint64_t acc = __shfl(excl, my_owner, 64);
   int qsel = 0;

@@ -30,7 +30,7 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 
 // LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows
 // (hot), lane-private offset sums, the bucket LUT
-constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8;
+constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8 + TILE * 8 + 16;
 // hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
 constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;
 

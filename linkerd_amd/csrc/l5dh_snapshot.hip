@@ -86,8 +86,8 @@ struct SrcLds32 {  // u32 row in LDS (half-tiles of big tiles), bins 1798/1799 z
 // tile is dirty, write the dense row(s), fold sumfix into the total and, in a
 // final snapshot, emit the HistogramSummary.  One wave.
 template <class SrcL>
-__device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_t vsum, bool dirty, bool keep,
-                                            int final_mode, State st, Tables tb, Outputs out) {
+__device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_t vsum, int64_t fix, bool dirty,
+                                            bool keep, int final_mode, State st, Tables tb, Outputs out) {
   const int lane = lane_id();
   const int ng = lane_groups(lane);
   const uint32_t oi = s - out.first;
@@ -127,12 +127,9 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
-  int64_t total = (int64_t)vsum + st.sumfix[s];
+  int64_t total = (int64_t)vsum + fix;  // fix = sumfix[s], read (and cleared) by the caller
   if (dirty) total += st.total[s];
-  if (lane == 0) {
-    st.sumfix[s] = 0;
-    if (keep) st.total[s] = total;
-  }
+  if (lane == 0 && keep) st.total[s] = total;
   if (emit) {
     Summary88* so = out.summ ? out.summ + oi : nullptr;
     if (dirty)
@@ -257,6 +254,8 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
     uint32_t* hist = smem;                    // [32][900] u16 pairs
     uint32_t* vsl = smem + TILE * CROW;       // [32][64] lane-private value sums (< 1152 x 2^21 per slot)
     uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);  // [LUT2_N]
+    int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the tile's series
+    uint32_t* dirtyl = reinterpret_cast<uint32_t*>(fixl + TILE);
     const int lane = lane_id();
     auto count = [&](uint32_t rec) {
       const uint32_t loc = (rec >> 21) & 31u;
@@ -278,6 +277,16 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
     if (one) {
       n0 = ld(g);
       n1 = ld(g + 4u * WG);
+    }
+    if (threadIdx.x < TILE) {  // the tile's sumfix entries (read and cleared here) and dirty flag
+      const uint32_t s = t * TILE + threadIdx.x;
+      int64_t f = 0;
+      if (s < st.S) {
+        f = st.sumfix[s];
+        if (f) st.sumfix[s] = 0;
+      }
+      fixl[threadIdx.x] = f;
+      if (threadIdx.x == 0) dirtyl[0] = st.dirty[t];
     }
     {
       uint4* p = reinterpret_cast<uint4*>(smem);
@@ -304,13 +313,13 @@ __global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State s
       for_tile_records(segs, t, 0, tot, count);
     }
     __syncthreads();
-    const bool dirty = st.dirty[t] != 0;
+    const bool dirty = dirtyl[0] != 0;
     for (int rep = 0; rep < 2; ++rep) {
       const uint32_t loc = w + 16 * rep;
       const uint32_t s = t * TILE + loc;
       if (s >= st.S) continue;
       const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
-      emit_series(SrcLds16{hist + loc * CROW}, s, vsum, dirty, keep, final_mode, st, tb, out);
+      emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dirty, keep, final_mode, st, tb, out);
     }
     if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
   }
@@ -362,7 +371,9 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   const uint32_t s = t * TILE + 16 * half + w;
   if (s < st.S) {
     if (single) {
-      emit_series(SrcLds32{hist + w * HROW}, s, my_vsum, st.dirty[t] != 0, keep, final_mode, st, tb, out);
+      const int64_t fix = st.sumfix[s];
+      if (lane == 0 && fix) st.sumfix[s] = 0;
+      emit_series(SrcLds32{hist + w * HROW}, s, my_vsum, fix, st.dirty[t] != 0, keep, final_mode, st, tb, out);
     } else {
       uint32_t* grow = st.counts + (size_t)s * ROW;
       const uint32_t* hrow = hist + w * HROW;
