@@ -155,6 +155,8 @@ struct l5dh_ctx {
   int num_cu = 256;
   uint32_t S = 0, F = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t side = nullptr;       // cold-tile accumulation runs here beside the hot tiles
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
   std::string last_error;
 
@@ -353,9 +355,23 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     HIPCHK(c, launch_hot_init(pl, hot, st, c->hot_chunk, c->stream));
   }
   {
+    // cold tiles on the side stream, concurrently with the hot tiles (disjoint
+    // tiles and series; the side stream joins back before anything reads them)
     KTimer kt(c, L5DH_K_ACCUM);
-    HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
-                           c->stream));
+    const bool split = cold_items && hot_items && !(c->dbg & 0x10000);
+    if (split) {
+      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      HIPCHK(c, launch_accum(sv, pl, cold_items, 0, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
+                             c->side));
+      HIPCHK(c, hipEventRecord(c->ev_join, c->side));
+      HIPCHK(c, launch_accum(sv, pl, 0, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
+                             c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    } else {
+      HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode,
+                             reset, c->stream));
+    }
   }
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
@@ -543,6 +559,10 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
   if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
+  if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+    return bail(-EIO);
   c->stream = c->own_stream;
   const size_t S = c->S, F = c->F;
   auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
@@ -606,6 +626,9 @@ int l5dh_close(l5dh_ctx* c) {
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->h_header) hipHostFree(c->h_header);
+  if (c->side) hipStreamDestroy(c->side);
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return 0;
