@@ -22,7 +22,6 @@ constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
-constexpr int B1_NT = 512;    // k_bin1 threads (2 workgroups per CU)
 constexpr int B2_NT = 256;
 constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
 constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
@@ -209,8 +208,8 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 // written in order.  Batches are < 2^30 samples.
 // LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, direct
 // words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
-template <int CH1, int WPS>
-__global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+template <int CH1, int NT, int WPS>
+__global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
@@ -232,8 +231,8 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
   const uint32_t TB = FS + ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
   const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
   const uint32_t* prow = pre + (size_t)blockIdx.x * F;
-  for (uint32_t w = threadIdx.x; w < NW; w += B1_NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
-  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += B1_NT) {
+  for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
+  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) {
     uint32_t sl = NHOT;
 #pragma unroll
     for (int q = 0; q < NHOT; ++q)
@@ -241,8 +240,8 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
     hslot[b] = (uint8_t)sl;
     cnt[b] = 0;
   }
-  for (uint32_t i = threadIdx.x; i < (NHOT + 1) * 64; i += B1_NT) hcnt[i] = 0;
-  for (uint32_t j = threadIdx.x; j < FS; j += B1_NT) {
+  for (uint32_t i = threadIdx.x; i < (NHOT + 1) * 64; i += NT) hcnt[i] = 0;
+  for (uint32_t j = threadIdx.x; j < FS; j += NT) {
     const uint32_t t0 = j * ST_TILES;
     const uint32_t t1 = min(F, t0 + ST_TILES);
     uint32_t acc = tile_base[t0];
@@ -250,7 +249,7 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
       if (!((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) acc += prow[t];
     oc[j] = make_uint2(0u, acc);
   }
-  for (uint32_t h = threadIdx.x; h < ND; h += B1_NT) {
+  for (uint32_t h = threadIdx.x; h < ND; h += NT) {
     const uint32_t t = plan[PLAN_DLIST + h];
     oc[FS + h] = make_uint2(0u, (tile_base[t] + prow[t]) | 0x80000000u);
   }
@@ -258,14 +257,14 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
-  constexpr int PT = CH1 / B1_NT;  // slots per thread: PT/4 groups of 4 consecutive
+  constexpr int PT = CH1 / NT;  // slots per thread: PT/4 groups of 4 consecutive
   for (size_t c0 = lo; c0 < hi; c0 += CH1) {
     uint32_t sv[PT];
     float fv[PT];
     if (vec && c0 + CH1 <= hi) {
 #pragma unroll
       for (int k = 0; k < PT / 4; ++k) {
-        const size_t base = c0 + 4 * ((size_t)k * B1_NT + threadIdx.x);
+        const size_t base = c0 + 4 * ((size_t)k * NT + threadIdx.x);
         const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
         const float4 f4 = *reinterpret_cast<const float4*>(values + base);
         sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
@@ -274,7 +273,7 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
     } else {
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        const size_t i = c0 + 4 * ((size_t)(k >> 2) * B1_NT + threadIdx.x) + (k & 3);
+        const size_t i = c0 + 4 * ((size_t)(k >> 2) * NT + threadIdx.x) + (k & 3);
         const bool in = i < hi;
         sv[k] = in ? series[i] : 0xFFFFFFFFu;
         fv[k] = in ? values[i] : 0.0f;
@@ -292,7 +291,7 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
     // direct words, branch-free bin selection, then one rank atomic per slot; hot
     // bins count in lane-private counters.
     uint32_t rec[PT];
-    uint32_t pk[PT];  // [12:0] local rank | [23:13] bin | [27:24] hot slot (NHOT: none)
+    uint32_t pk[PT];  // [13:0] local rank | [24:14] bin | [28:25] hot slot (NHOT: none)
 #pragma unroll
     for (int g = 0; g < PT; g += 4) {
       uint32_t pl[4];
@@ -338,7 +337,7 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
       for (int q = 0; q < 4; ++q) {
         const bool hot = sl[q] < (uint32_t)NHOT;
         uint32_t* ctr = hot ? hcnt + sl[q] * 64u + (uint32_t)lane : cnt + bn[q];
-        pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 13) | (sl[q] << 24);
+        pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
@@ -373,21 +372,21 @@ __global__ __launch_bounds__(B1_NT, WPS) void k_bin1(const uint32_t* __restrict_
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      const uint32_t bin = (pk[k] >> 13) & 2047u;
-      const uint32_t r = (pk[k] & 8191u) + hcnt[(pk[k] >> 24) * 64 + lane];  // row NHOT is zero
+      const uint32_t bin = (pk[k] >> 14) & 2047u;
+      const uint32_t r = (pk[k] & 16383u) + hcnt[(pk[k] >> 25) * 64 + lane];  // row NHOT is zero
       const uint2 x = oc[bin];
       stage[x.x + r] = make_uint2(rec[k], x.y + r);
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < TB; j += B1_NT) {  // cursors advance; the stage carries the destinations
+    for (uint32_t j = threadIdx.x; j < TB; j += NT) {  // cursors advance; the stage carries the destinations
       oc[j].y += cnt[j];
       cnt[j] = 0;
     }
     if (threadIdx.x == 0) cnt[TB] = 0;
-    for (uint32_t i = threadIdx.x; i < NHOT * 64; i += B1_NT) hcnt[i] = 0;
+    for (uint32_t i = threadIdx.x; i < NHOT * 64; i += NT) hcnt[i] = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
-      const uint2 e = stage[threadIdx.x + k * B1_NT];
+      const uint2 e = stage[threadIdx.x + k * NT];
       if (!(dbg & 1)) ((e.y >> 31) ? records : out1)[e.y & 0x7FFFFFFFu] = e.x;
     }
     __syncthreads();
@@ -698,9 +697,13 @@ hipError_t set_ingest_attributes() {
   const int big = 160 * 1024;
   if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bin1_lds(6144))))
     return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bin1_lds(16384))))
+    return e;
+
 
   return hipSuccess;
 }
@@ -742,8 +745,15 @@ hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* 
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
                        uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
-  hipLaunchKernelGGL((k_bin1<6144, 4>), dim3(G), dim3(B1_NT), bin1_lds(6144), st, series, values, n, per, S, F, pre,
-                     tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+  // sub-chunk size x workgroup: (16384 slots, 1024 threads, 1 workgroup/CU) by
+  // default -- longer runs per bin beat the second workgroup's overlap (measured);
+  // L5DH_DBG bit 20 selects (6144, 512, 2 workgroups/CU)
+  if ((dbg >> 20) & 1)
+    hipLaunchKernelGGL((k_bin1<6144, 512, 4>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
+                       pre, tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+  else
+    hipLaunchKernelGGL((k_bin1<16384, 1024, 4>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
+                       F, pre, tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
 

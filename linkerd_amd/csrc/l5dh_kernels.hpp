@@ -96,7 +96,7 @@ constexpr int DIRECT_MAX = 512;
 constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + direct tiles (<= 512)
 // k_bin1 LDS for a sub-chunk of ch slots: stage, cnt, oc, direct words + prefixes, hot slots, hot counters
 constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4; }
-constexpr size_t BIN1_SCRATCH_PAD = 6144 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
+constexpr size_t BIN1_SCRATCH_PAD = 16384 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
 constexpr int PLAN_WORDS = 8192;
 constexpr int PLAN_HINT = 2040;     // [2] hot-tile hints for the next batch's k_count
