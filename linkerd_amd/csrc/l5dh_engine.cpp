@@ -173,11 +173,15 @@ struct l5dh_ctx {
   uint8_t* d_dirty = nullptr;
   uint32_t* d_err = nullptr;
   // scratch
-  uint32_t* d_table = nullptr;  // [G_max][F]
-  uint32_t* d_tile_tot = nullptr;
+  uint32_t* d_table = nullptr;  // [G_max][F + COLS]
+  uint32_t* d_tile_tot = nullptr;  // [F + COLS] column totals (ingest), tile totals (snapshot plan)
   uint32_t* d_cold_tile = nullptr;
-  DevBuf hot_item;  // big-tile chunk items (sized per snapshot)
+  DevBuf hot_item;    // big-tile chunk items (sized per snapshot)
+  DevBuf split_item;  // split-tile half chunk items (sized per snapshot)
   uint32_t* d_hot_list = nullptr;
+  uint8_t* d_tile_flags = nullptr;
+  uint32_t* d_nosplit = nullptr;  // empty split set [SPLIT_SLOT] (single-level batches)
+  int split_cur = 0;              // split-set slot of the next batch in d_b2plan + PLAN_SPLIT
   uint32_t* d_header = nullptr;
   uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
   uint32_t* h_header = nullptr;  // pinned
@@ -186,6 +190,7 @@ struct l5dh_ctx {
   struct Seg {
     DevBuf recs;
     uint32_t* tbase = nullptr;
+    uint32_t* sinfo = nullptr;  // [sinfo_words(F)] split tiles of the batch and their half-0 records
     size_t n = 0;
   };
   Seg segs[MAX_SEG];
@@ -314,7 +319,8 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot, c->d_cold_tile, static_cast<uint32_t*>(c->hot_item.p), c->d_hot_list, c->d_header};
+  return Plan{c->d_tile_tot,   c->d_cold_tile,   static_cast<uint32_t*>(c->hot_item.p), static_cast<uint2*>(c->split_item.p),
+              c->d_hot_list, c->d_tile_flags, c->d_header};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -323,6 +329,7 @@ Segs segs_view(l5dh_ctx* c) {
   for (int j = 0; j < c->nseg; ++j) {
     s.recs[j] = static_cast<const uint32_t*>(c->segs[j].recs.p);
     s.tbase[j] = c->segs[j].tbase;
+    s.sinfo[j] = c->segs[j].sinfo;
   }
   return s;
 }
@@ -335,7 +342,8 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   {
     size_t recs = 0;
     for (int j = 0; j < c->nseg; ++j) recs += c->segs[j].n;
-    const int r = ensure(c, c->hot_item, (recs / c->hot_chunk + c->F + 1) * 4);
+    int r = ensure(c, c->hot_item, (recs / c->hot_chunk + c->F + 1) * 4);
+    if (!r) r = ensure(c, c->split_item, (recs / c->hot_chunk + 2 * (size_t)c->F + 2) * 8);
     if (r) return r;
   }
   Plan pl = plan(c);
@@ -343,11 +351,12 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, pl, c->stream));
   }
-  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 12, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 16, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint32_t cold_items = c->h_header[0];
   const uint32_t hot = c->h_header[1];
   const uint32_t hot_items = c->h_header[2];
+  const uint32_t split_items = c->h_header[3];
   State st = state(c);
   Tables tb = tables(c);
   if (hot) {
@@ -358,17 +367,20 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     // cold tiles on the side stream, concurrently with the hot tiles (disjoint
     // tiles and series; the side stream joins back before anything reads them)
     KTimer kt(c, L5DH_K_ACCUM);
-    const bool split = cold_items && hot_items && !(c->dbg & 0x10000);
-    if (split) {
+    const bool two = cold_items && (hot_items || split_items) && !(c->dbg & 0x10000);
+    if (two) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
       HIPCHK(c, launch_accum(sv, pl, cold_items, 0, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
                              c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-      HIPCHK(c, launch_accum(sv, pl, 0, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
-                             c->stream));
+      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, c->hot_chunk, c->stream));
+      if (hot_items)
+        HIPCHK(c, launch_accum(sv, pl, 0, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode, reset,
+                               c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
+      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, c->hot_chunk, c->stream));
       HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, c->hot_chunk, final_mode,
                              reset, c->stream));
     }
@@ -428,29 +440,36 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   per = (per + 3) & ~(size_t)3;
   G = (int)((n + per - 1) / per);
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
+  const bool two_level = c->bin_mode != 1;
+  // split set of this batch (chosen from the previous batch's tile totals) and of the next
+  uint32_t* split_slot = c->d_b2plan + PLAN_SPLIT;
+  const uint32_t* cur = two_level ? split_slot + c->split_cur * SPLIT_SLOT : c->d_nosplit;
+  uint32_t* nxt = split_slot + (c->split_cur ^ 1) * SPLIT_SLOT;
   {
     KTimer kt(c, L5DH_K_COUNT);
-    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + PLAN_HINT, vec, c->stream));
+    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + PLAN_HINT, cur, vec,
+                           c->stream));
   }
   {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_colscan(c->d_table, G, c->F, c->d_tile_tot, c->stream));
-    HIPCHK(c, launch_tilescan(c->d_tile_tot, c->F, sg.tbase, c->stream));
+    HIPCHK(c, launch_tilescan(c->d_tile_tot, c->F, cur, sg.tbase, c->stream));
+    HIPCHK(c, launch_seginfo(cur, c->d_tile_tot, c->F, sg.sinfo, c->stream));
   }
-  const bool two_level = c->bin_mode != 1;
   if (two_level) {
     int r = ensure(c, c->scratch1, (n + BIN1_SCRATCH_PAD) * 4);  // trash bin; k_bin2 reads whole 16-B groups
     if (r) return r;
     {
       KTimer kt(c, L5DH_K_SCAN);
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
-      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull),
-                              c->direct_max, c->stream));
+      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
+                              (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->stream));
+      c->split_cur ^= 1;
     }
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
-                            static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
+                            c->d_tile_tot, static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
                             c->dbg, c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
@@ -569,11 +588,13 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
-            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * F * 4) &&
-            mal((void**)&c->d_tile_tot, F * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
+            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * (F + COLS) * 4) &&
+            mal((void**)&c->d_tile_tot, (F + COLS) * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
-            mal((void**)&c->d_b2plan, 4 * PLAN_WORDS);
-  for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4);
+            mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
+            mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT);
+  for (int j = 0; ok && j < MAX_SEG; ++j)
+    ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4) && mal((void**)&c->segs[j].sinfo, sinfo_words(c->F) * 4);
   if (!ok) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
@@ -597,7 +618,9 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
-      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * PLAN_WORDS) != hipSuccess ||
+      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * PLAN_SPLIT) != hipSuccess ||
+      hipMemset(c->d_b2plan + PLAN_SPLIT, 0, 4 * 2 * SPLIT_SLOT) != hipSuccess ||
+      hipMemset(c->d_nosplit, 0, 4 * SPLIT_SLOT) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
   *out = c;
@@ -614,14 +637,15 @@ int l5dh_close(l5dh_ctx* c) {
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
-                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan};
+                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan, c->d_tile_flags, c->d_nosplit};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
     if (s.tbase) hipFree(s.tbase);
+    if (s.sinfo) hipFree(s.sinfo);
     if (s.recs.p) hipFree(s.recs.p);
   }
-  DevBuf* bufs[] = {&c->scratch1, &c->hot_item, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
+  DevBuf* bufs[] = {&c->scratch1, &c->hot_item, &c->split_item, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
                     &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);

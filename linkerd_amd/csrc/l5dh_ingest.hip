@@ -27,17 +27,31 @@ constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
 constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
 
 // ------------------------------------------------------------------------
+// Count key of a valid sample: its tile, or for a split tile the column of its
+// half (F + 2 s + half).  sw[w] = {split bits of word w, split tiles before it}.
+__device__ __forceinline__ uint32_t count_key(uint32_t s, uint32_t F, uint2 sw) {
+  const uint32_t t = s >> TILE_SHIFT;
+  const uint32_t bit = 1u << (t & 31u);
+  const uint32_t sk = F + 2u * (sw.y + (uint32_t)__popc(sw.x & (bit - 1u))) + ((s >> 4) & 1u);
+  return (sw.x & bit) ? sk : t;
+}
+
 __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ series, size_t n, size_t per, uint32_t S,
                                               uint32_t F, uint32_t* __restrict__ table, uint32_t* __restrict__ err,
-                                              const uint32_t* __restrict__ hint, int vec) {
+                                              const uint32_t* __restrict__ hint, const uint32_t* __restrict__ split,
+                                              int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* cnt = smem;
-  for (uint32_t t = threadIdx.x; t < F; t += WG) cnt[t] = 0;
+  const uint32_t C = F + COLS;
+  uint2* sw = reinterpret_cast<uint2*>(smem);  // [1024] split words
+  uint32_t* cnt = smem + 2048;                  // [C]
+  const uint32_t NW = (F + 31) / 32;
+  for (uint32_t t = threadIdx.x; t < C; t += WG) cnt[t] = 0;
+  for (uint32_t w = threadIdx.x; w < NW; w += WG) sw[w] = make_uint2(split[SPLIT_BITS + w], split[SPLIT_PRE + w]);
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
-  const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot tiles of the previous batch (aggregation only)
-  const uint32_t hk[2] = {hot0, hot1};
+  const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot columns of the previous batch (aggregation only)
+  const uint32_t hk[2] = {hot0 < C ? hot0 : 0xFFFFFFFFu, hot1 < C ? hot1 : 0xFFFFFFFFu};
   bool bad = false;
   if (lo < hi) {
     size_t done = lo;
@@ -49,12 +63,15 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       for (; wlast - threadIdx.x + i + 3 * WG < nv; i += 4 * WG) {
         const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
         const uint32_t sv[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+        uint2 wv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) wv[k] = sw[min(sv[k], S - 1) >> (TILE_SHIFT + 5)];
         uint32_t key[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const bool ok = sv[k] < S;
           bad |= !ok;
-          key[k] = ok ? sv[k] >> TILE_SHIFT : 0xFFFFFFFFu;
+          key[k] = ok ? count_key(sv[k], F, wv[k]) : 0xFFFFFFFFu;
         }
         hot_inc_batch<2, 16>(cnt, key, hk);
       }
@@ -65,7 +82,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
         auto one_in = [&](uint32_t s) {
           const bool ok = in && s < S;
           bad |= in && !ok;
-          hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
+          hot_inc(cnt, ok ? count_key(s, F, sw[s >> (TILE_SHIFT + 5)]) : 0u, ok, hk[0], hk[1]);
         };
         one_in(a.x); one_in(a.y); one_in(a.z); one_in(a.w);
       }
@@ -76,17 +93,17 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const uint32_t s = i < hi ? series[i] : 0xFFFFFFFFu;
       const bool ok = s < S;
       bad |= i < hi && !ok;
-      hot_inc(cnt, s >> TILE_SHIFT, ok, hot0, hot1);
+      hot_inc(cnt, ok ? count_key(s, F, sw[s >> (TILE_SHIFT + 5)]) : 0u, ok, hk[0], hk[1]);
     }
   }
   if (bad) atomicOr(err, 1u);
   __syncthreads();
-  uint32_t* row = table + (size_t)blockIdx.x * F;
-  for (uint32_t t = threadIdx.x; t < F; t += WG) row[t] = cnt[t];
+  uint32_t* row = table + (size_t)blockIdx.x * C;
+  for (uint32_t t = threadIdx.x; t < C; t += WG) row[t] = cnt[t];
 }
 
 // WG = 64 tiles x 16 slab groups.
-__global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, int G, uint32_t F,
+__global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, int G, uint32_t C,
                                                   uint32_t* __restrict__ tile_tot) {
   __shared__ uint32_t part[16][64];
   const int lane = threadIdx.x & 63;
@@ -96,8 +113,8 @@ __global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, 
   const int g0 = w * gper;
   const int g1 = min(G, g0 + gper);
   uint32_t s = 0;
-  if (t < F)
-    for (int g = g0; g < g1; ++g) s += table[(size_t)g * F + t];
+  if (t < C)
+    for (int g = g0; g < g1; ++g) s += table[(size_t)g * C + t];
   part[w][lane] = s;
   __syncthreads();
   if (w == 0) {
@@ -107,13 +124,13 @@ __global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, 
       part[k][lane] = acc;
       acc += v;
     }
-    if (t < F) tile_tot[t] = acc;
+    if (t < C) tile_tot[t] = acc;
   }
   __syncthreads();
-  if (t < F) {
+  if (t < C) {
     uint32_t acc = part[w][lane];
     for (int g = g0; g < g1; ++g) {
-      const size_t i = (size_t)g * F + t;
+      const size_t i = (size_t)g * C + t;
       const uint32_t v = table[i];
       table[i] = acc;
       acc += v;
@@ -121,22 +138,51 @@ __global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, 
   }
 }
 
-__global__ __launch_bounds__(1024) void k_tilescan(const uint32_t* __restrict__ tile_tot, uint32_t F,
-                                                   uint32_t* __restrict__ tile_base) {
+// Tile totals (a split tile's own column is empty: its total is its two half
+// columns, written back to coltot[t]) and their exclusive scan tile_base[F+1].
+__global__ __launch_bounds__(1024) void k_tilescan(uint32_t* __restrict__ coltot, uint32_t F,
+                                                   const uint32_t* __restrict__ split, uint32_t* __restrict__ tile_base) {
   __shared__ uint32_t lds[17];
   const uint32_t per = (F + 1023) / 1024;
   const uint32_t t0 = threadIdx.x * per;
   uint32_t s = 0;
-  for (uint32_t k = 0; k < per; ++k)
-    if (t0 + k < F) s += tile_tot[t0 + k];
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t t = t0 + k;
+    if (t >= F) break;
+    const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
+    const uint32_t bit = 1u << (t & 31u);
+    uint32_t v = coltot[t];
+    if (wd & bit) {
+      const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
+      v += coltot[F + 2 * si] + coltot[F + 2 * si + 1];
+      coltot[t] = v;
+    }
+    s += v;
+  }
   uint32_t tot;
   uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
   for (uint32_t k = 0; k < per; ++k)
     if (t0 + k < F) {
       tile_base[t0 + k] = acc;
-      acc += tile_tot[t0 + k];
+      acc += coltot[t0 + k];
     }
   if (threadIdx.x == 0) tile_base[F] = tot;
+}
+
+// Segment split info (l5dh_kernels.hpp) from the batch's split set.
+__global__ __launch_bounds__(1024) void k_seginfo(const uint32_t* __restrict__ split, const uint32_t* __restrict__ coltot,
+                                                  uint32_t F, uint32_t* __restrict__ sinfo) {
+  const uint32_t NS = split[0];
+  uint16_t* map = reinterpret_cast<uint16_t*>(sinfo + SINFO_MAP);
+  for (uint32_t t = threadIdx.x; t < F; t += 1024) map[t] = NO_SPLIT;
+  __syncthreads();
+  if (threadIdx.x == 0) sinfo[0] = NS;
+  for (uint32_t si = threadIdx.x; si < NS; si += 1024) {
+    const uint32_t t = split[SPLIT_LIST + si];
+    sinfo[1 + si] = t;
+    sinfo[SINFO_H0 + si] = coltot[F + 2 * si];
+    map[t] = (uint16_t)si;
+  }
 }
 
 // Level-1 payload of a sample outside [0, V_ESC): bucketize, add its exact
@@ -165,7 +211,7 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
                                             int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* cur = smem;
-  const uint32_t* row = table + (size_t)blockIdx.x * F;
+  const uint32_t* row = table + (size_t)blockIdx.x * (F + COLS);  // counted without split tiles
   for (uint32_t t = threadIdx.x; t < F; t += WG) cur[t] = tile_base[t] + row[t];
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
@@ -194,8 +240,9 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 // ------------------------------------------------------------------------
 // Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
 
-// Level 1.  Bins = the FS super-tiles (records of their non-direct tiles, into
-// scratch1) and the ND direct tiles (records straight into the final layout), plus a trash bin for sample slots with no sample (batch
+// Level 1.  Bins = the FS super-tiles (records of their non-split tiles, into
+// scratch1) and both halves of the ND split tiles (records straight into the
+// final layout: half 0 from the tile's start, half 1 after all half-0 records), plus a trash bin for sample slots with no sample (batch
 // tail, ids >= S: counted as errors by k_count) written to scratch1[n ..).  Both
 // arrays share the final layout's index space: slab g's records of direct tile t
 // start at tile_base[t] + pre[g][t]; its level-1 records of super-tile j at
@@ -213,9 +260,9 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
-                                                const uint32_t* __restrict__ plan, uint32_t* __restrict__ out1,
-                                                uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
-                                                int vec, int dbg) {
+                                                const uint32_t* __restrict__ plan, const uint32_t* __restrict__ coltot,
+                                                uint32_t* __restrict__ out1, uint32_t* __restrict__ records,
+                                                int64_t* __restrict__ sumfix, int vec, int dbg) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
   uint32_t* cnt = smem + 2 * CH1;                                  // [BIN1_BINS]
@@ -228,9 +275,9 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
   const uint32_t ND = plan[PLAN_ND];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const uint32_t TB = FS + ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
+  const uint32_t TB = FS + 2 * ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
   const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
-  const uint32_t* prow = pre + (size_t)blockIdx.x * F;
+  const uint32_t* prow = pre + (size_t)blockIdx.x * (F + COLS);
   for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
   for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) {
     uint32_t sl = NHOT;
@@ -249,9 +296,11 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       if (!((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) acc += prow[t];
     oc[j] = make_uint2(0u, acc);
   }
-  for (uint32_t h = threadIdx.x; h < ND; h += NT) {
-    const uint32_t t = plan[PLAN_DLIST + h];
-    oc[FS + h] = make_uint2(0u, (tile_base[t] + prow[t]) | 0x80000000u);
+  for (uint32_t h = threadIdx.x; h < 2 * ND; h += NT) {  // split tile h/2: half 0 from its start, half 1 after it
+    const uint32_t si = h >> 1;
+    const uint32_t t = plan[PLAN_DLIST + si];
+    const uint32_t at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + h];
+    oc[FS + h] = make_uint2(0u, at | 0x80000000u);
   }
   if (threadIdx.x == 0) oc[TB] = make_uint2(0u, trash);
   __syncthreads();
@@ -328,7 +377,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         const uint32_t bit = 1u << (t & 31u);
         const bool direct = (dv[q].x & bit) != 0u;
         rec[g + q] = ((t & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl[q];
-        const uint32_t dbin = FS + dv[q].y + (uint32_t)__popc(dv[q].x & (bit - 1u));
+        const uint32_t dbin = FS + 2u * (dv[q].y + (uint32_t)__popc(dv[q].x & (bit - 1u))) + ((s >> 4) & 1u);
         bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
       }
 #pragma unroll
@@ -396,27 +445,29 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 // Ingest plan (one workgroup, after the tile totals are known):
 //   plan[0..FS]          level-2 item_start per super-tile (nb_j items of equal
 //                        slab ranges, ~B2_ITEM level-1 records each: skew-balanced;
-//                        0 items for a super-tile whose tiles are all direct/empty)
+//                        0 items for a super-tile whose tiles are all split/empty)
 //   plan[FS+1 .. 2FS]    slab-range size per super-tile
-//   plan[2FS+1 .. 3FS]   hot non-direct tiles of the super-tile (tile-in-ST, byte 0
+//   plan[2FS+1 .. 3FS]   hot non-split tiles of the super-tile (tile-in-ST, byte 0
 //                        and 1; 0xFF = none): >= 1/8 of its level-1 records
-//   plan[3FS+1 .. +NHOT] hot k_bin1 bins (>= 1/64 of all records, or ~0u)
-//   plan[PLAN_DBITS..]   direct tiles (bitmap, word prefixes, list, count)
-//   plan[PLAN_HINT..+1]  hot-tile hints for the next batch's k_count
-__global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ tile_tot,
-                                                 uint32_t* __restrict__ plan, uint32_t thr_min, uint32_t dmax) {
+//   plan[3FS+1 .. +NHOT] hot k_bin1 bins (>= 1/128 of all records, or ~0u)
+//   plan[PLAN_DBITS..]   this batch's split tiles (copy of slot `cur`)
+//   nxt                  the next batch's split set
+//   plan[PLAN_HINT..+1]  hot count columns for the next batch's k_count
+__global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
+                                                 uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
+                                                 uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax) {
   __shared__ uint32_t lds[17];
   __shared__ unsigned long long best[16];
   __shared__ uint32_t lhist[33];
   __shared__ uint32_t sthr;
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t j = threadIdx.x;
-  // direct threshold: smallest power of two (>= thr_min) selecting <= dmax tiles
+  // next split set: smallest power of two (>= thr_min) selecting <= dmax tiles
   if (j < 33) lhist[j] = 0;
   __syncthreads();
   if (dmax > 0)
     for (uint32_t t = j; t < F; t += 1024) {
-      const uint32_t v = tile_tot[t];
+      const uint32_t v = coltot[t];
       if (v >= thr_min && v > 0) atomicAdd(&lhist[31 - __clz((int)v)], 1u);
     }
   __syncthreads();
@@ -438,28 +489,31 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   }
   __syncthreads();
   const uint32_t thr = sthr;
-  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nd = 0, w0 = 0, w1 = 0;
+  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nn = 0, n0 = 0, n1 = 0;
+  uint32_t c0 = 0, c1 = 0;  // this batch's split words of the super-tile
   uint64_t ctot = 0, tot = 0;
   unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile): this thread's two biggest tiles
   if (j < FS) {
+    c0 = cur[SPLIT_BITS + 2 * j];
+    c1 = 2 * j + 1 < 1024 ? cur[SPLIT_BITS + 2 * j + 1] : 0u;
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest non-direct tiles of this super-tile
+    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest non-split tiles of this super-tile
     uint32_t a0 = 0, a1 = 0, k0 = 0xFF, k1 = 0xFF;  // two biggest tiles
     for (uint32_t t = j * ST_TILES; t < t1; ++t) {
-      const uint32_t v = tile_tot[t];
+      const uint32_t v = coltot[t];
       const uint32_t tl = t - j * ST_TILES;
       tot += v;
       if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
       else if (v > a1) { a1 = v; k1 = tl; }
       if (v >= thr) {
-        if (tl < 32) w0 |= 1u << tl; else w1 |= 1u << (tl - 32);
-        continue;
+        if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
       }
+      if (((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u) continue;  // split now: no level-1 records
       ctot += v;
       if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
       else if (v > b1) { b1 = v; i1 = tl; }
     }
-    nd = (uint32_t)(__popc(w0) + __popc(w1));
+    nn = (uint32_t)(__popc(n0) + __popc(n1));
     tkA = k0 != 0xFF ? (((unsigned long long)a0 << 16) | (j * ST_TILES + k0)) : 0ull;
     tkB = k1 != 0xFF ? (((unsigned long long)a1 << 16) | (j * ST_TILES + k1)) : 0ull;
     if ((uint64_t)b0 * 8 < ctot || b0 == 0) i0 = 0xFF;
@@ -474,9 +528,9 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       gsz = (uint32_t)G;
     }
   }
-  uint32_t total, ndt;
+  uint32_t total, nnt;
   const uint32_t e = block_excl_scan<1024>(nb, lds, &total);
-  const uint32_t de = block_excl_scan<1024>(nd, lds, &ndt);
+  const uint32_t ne = block_excl_scan<1024>(nn, lds, &nnt);
   // this thread's NHOT biggest k_bin1 bins, descending: (records << 11 | bin)
   unsigned long long bk[NHOT] = {};
   auto push = [&](unsigned long long k) {
@@ -492,31 +546,49 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     plan[j] = e;
     plan[FS + 1 + j] = gsz;
     plan[2 * FS + 1 + j] = hot;
-    plan[PLAN_DBITS + 2 * j] = w0;
-    plan[PLAN_DPRE + 2 * j] = de;
+    // this batch's split tiles (copied for k_bin1 / k_bin2) and their half bins
+    plan[PLAN_DBITS + 2 * j] = c0;
+    plan[PLAN_DPRE + 2 * j] = cur[SPLIT_PRE + 2 * j];
     if (2 * j + 1 < 1024) {
-      plan[PLAN_DBITS + 2 * j + 1] = w1;
-      plan[PLAN_DPRE + 2 * j + 1] = de + (uint32_t)__popc(w0);
+      plan[PLAN_DBITS + 2 * j + 1] = c1;
+      plan[PLAN_DPRE + 2 * j + 1] = cur[SPLIT_PRE + 2 * j + 1];
     }
-    uint32_t h = de;
+    uint32_t si = cur[SPLIT_PRE + 2 * j];
     for (int q = 0; q < 2; ++q) {
-      uint32_t w = q ? w1 : w0;
+      uint32_t w = q ? c1 : c0;
       while (w) {
         const uint32_t tl = (uint32_t)(__ffs((int)w) - 1) + 32u * q;
         w &= w - 1u;
-        const uint32_t t = j * ST_TILES + tl;
-        plan[PLAN_DLIST + h] = t;
-        push(((unsigned long long)tile_tot[t] << 11) | (FS + h));
-        ++h;
+        plan[PLAN_DLIST + si] = j * ST_TILES + tl;
+        push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * si));
+        push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * si + 1));
+        ++si;
       }
     }
     if (ctot) push((ctot << 11) | j);
+    // the next batch's split set
+    nxt[SPLIT_BITS + 2 * j] = n0;
+    nxt[SPLIT_PRE + 2 * j] = ne;
+    if (2 * j + 1 < 1024) {
+      nxt[SPLIT_BITS + 2 * j + 1] = n1;
+      nxt[SPLIT_PRE + 2 * j + 1] = ne + (uint32_t)__popc(n0);
+    }
+    uint32_t h = ne;
+    for (int q = 0; q < 2; ++q) {
+      uint32_t w = q ? n1 : n0;
+      while (w) {
+        const uint32_t tl = (uint32_t)(__ffs((int)w) - 1) + 32u * q;
+        w &= w - 1u;
+        nxt[SPLIT_LIST + h++] = j * ST_TILES + tl;
+      }
+    }
   }
   if (threadIdx.x == 0) {
     plan[FS] = total;
-    plan[PLAN_ND] = ndt;
+    plan[PLAN_ND] = cur[0];
+    nxt[0] = nnt;
   }
-  // grand total, the two biggest bins and the two biggest tiles (block reductions)
+  // grand total, the hot bins and the two biggest tiles (block reductions)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   auto block_reduce = [&](unsigned long long v, bool is_max) -> unsigned long long {
 #pragma unroll
@@ -551,12 +623,27 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       const uint64_t v = ks[h] >> 11;
       plan[3 * FS + 1 + h] = (v > 0 && v * 128 >= grand) ? (uint32_t)(ks[h] & 2047u) : NOKEY;
     }
-    // hot-tile hints for the next batch's k_count (tiles with >= 1/64 of the records)
+    // next batch's k_count hints: the count columns of the two biggest tiles
+    // (both halves of the biggest one when it will be split); aggregation only
+    uint32_t hkey[2] = {NOKEY, NOKEY};
+    int nh = 0;
     const unsigned long long ts[2] = {t1, t2};
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t v = ts[h] >> 16;
-      plan[PLAN_HINT + h] = (v > 0 && v * 64 >= grand) ? (uint32_t)(ts[h] & 0xFFFFu) : NOKEY;
+    for (int q = 0; q < 2 && nh < 2; ++q) {
+      const uint64_t v = ts[q] >> 16;
+      if (v == 0 || v * 64 < grand) continue;
+      const uint32_t t = (uint32_t)(ts[q] & 0xFFFFu);
+      const uint32_t wd = nxt[SPLIT_BITS + (t >> 5)];  // written above by this workgroup
+      const uint32_t bit = 1u << (t & 31u);
+      if (wd & bit) {
+        const uint32_t si = nxt[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
+        hkey[nh++] = F + 2 * si;
+        if (nh < 2) hkey[nh++] = F + 2 * si + 1;
+      } else {
+        hkey[nh++] = t;
+      }
     }
+    plan[PLAN_HINT] = hkey[0];
+    plan[PLAN_HINT + 1] = hkey[1];
   }
 }
 
@@ -598,9 +685,9 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     if ((uint32_t)lane < nt) {
       const uint32_t t = t0 + lane;
       const bool direct = (plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u;
-      p0 = pre[(size_t)g0 * F + t];
+      p0 = pre[(size_t)g0 * (F + COLS) + t];
       cur[lane] = tile_base[t] + p0;
-      p1 = g1 < G ? pre[(size_t)g1 * F + t] : (tile_base[t + 1] - tile_base[t]);
+      p1 = g1 < G ? pre[(size_t)g1 * (F + COLS) + t] : (tile_base[t + 1] - tile_base[t]);
       if (direct) p0 = p1 = 0;  // its records never reach level 1
     }
     cnt[lane] = 0;
@@ -709,51 +796,58 @@ hipError_t set_ingest_attributes() {
 }
 
 hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
-                        uint32_t* table, uint32_t* err, const uint32_t* hint, bool vec, hipStream_t st) {
-  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), (size_t)F * 4, st, series, n, per, S, F, table, err, hint,
-                     vec ? 1 : 0);
+                        uint32_t* table, uint32_t* err, const uint32_t* hint, const uint32_t* split, bool vec,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), ((size_t)F + COLS + 2048) * 4, st, series, n, per, S, F, table, err,
+                     hint, split, vec ? 1 : 0);
   return hipGetLastError();
 }
 
-hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* tile_tot, hipStream_t st) {
-  hipLaunchKernelGGL(k_colscan, dim3((F + 63) / 64), dim3(1024), 0, st, table, G, F, tile_tot);
+hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* coltot, hipStream_t st) {
+  hipLaunchKernelGGL(k_colscan, dim3((F + COLS + 63) / 64), dim3(1024), 0, st, table, G, F + COLS, coltot);
   return hipGetLastError();
 }
 
-hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_base, hipStream_t st) {
-  hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(1024), 0, st, tile_tot, F, tile_base);
+hipError_t launch_tilescan(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base, hipStream_t st) {
+  hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(1024), 0, st, coltot, F, split, tile_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st) {
+  hipLaunchKernelGGL(k_seginfo, dim3(1), dim3(1024), 0, st, split, coltot, F, sinfo);
   return hipGetLastError();
 }
 
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
                       int64_t* sumfix, bool vec, hipStream_t st) {
-  const size_t lds = (size_t)F * 4;
+  const size_t lds = (size_t)F * 4;  // the batch was counted without split tiles (tile columns only)
   hipLaunchKernelGGL(k_bin, dim3(G), dim3(WG), lds, st, series, values, n, per, S, F, table, tile_base, tb, records,
                      sumfix, vec ? 1 : 0);
   return hipGetLastError();
 }
 
-hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, uint32_t thr_min,
-                         uint32_t dmax, hipStream_t st) {
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, hipStream_t st) {
   const uint32_t FS = (F + 63) / 64;
-  const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, (uint32_t)BIN1_BINS - 1 - FS);  // + trash bin
-  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, tile_tot, stplan, thr_min, std::min(dmax, cap));
+  const uint32_t cap = std::min<uint32_t>((uint32_t)SPLIT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
+  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap));
   return hipGetLastError();
 }
 
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
+                       const uint32_t* coltot, uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg,
+                       hipStream_t st) {
   // sub-chunk size x workgroup: (16384 slots, 1024 threads, 1 workgroup/CU) by
   // default -- longer runs per bin beat the second workgroup's overlap (measured);
   // L5DH_DBG bit 20 selects (6144, 512, 2 workgroups/CU)
   if ((dbg >> 20) & 1)
     hipLaunchKernelGGL((k_bin1<6144, 512, 4>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
-                       pre, tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+                       pre, tile_base, tb, stplan, coltot, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   else
     hipLaunchKernelGGL((k_bin1<16384, 1024, 4>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
-                       F, pre, tile_base, tb, stplan, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+                       F, pre, tile_base, tb, stplan, coltot, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 // (hot), lane-private offset sums, the bucket LUT
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8 + TILE * 8 + 16;
 // hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
+constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
 constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;
 
 constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
@@ -45,9 +46,24 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
   const uint2* lut2;       // [LUT2_N] {o1 | o2 << 16, b0 | p << 16} (bucket_lut2)
 };
 
+// Split tiles: the hottest tiles of the previous batch (<= SPLIT_MAX) are counted,
+// binned and laid out per half-tile (series 0-15 | 16-31): a split tile's region
+// holds its half-0 records first, then its half-1 records, so the big-tile
+// accumulation reads each half as one contiguous range.
+constexpr int SPLIT_MAX = 255;
+constexpr int COLS = 2 * SPLIT_MAX;   // count-table columns past F: the half counters of split tiles
+// Split-set slot (SPLIT_SLOT u32): [0] NS | [1 + s] tile id (ascending) | bitmap | word prefixes
+constexpr int SPLIT_LIST = 1, SPLIT_BITS = 256, SPLIT_PRE = 1280, SPLIT_SLOT = 2304;
+// Per-segment split info (SINFO_WORDS(F) u32): [0] NS | [1 + s] tile | [256 + s] half-0 records
+// | u16 map tile -> s (0xFFFF: not split) from word 512
+constexpr int SINFO_H0 = 256, SINFO_MAP = 512;
+constexpr size_t sinfo_words(uint32_t F) { return SINFO_MAP + (F + 1) / 2 + 1; }
+constexpr uint16_t NO_SPLIT = 0xFFFF;
+
 struct Segs {              // binned ingest batches awaiting aggregation
   const uint32_t* recs[MAX_SEG];
   const uint32_t* tbase[MAX_SEG];  // [F+1] record offset of each tile
+  const uint32_t* sinfo[MAX_SEG];  // split info of the segment
   int n;
 };
 
@@ -65,12 +81,17 @@ struct State {
   uint32_t S, F;
 };
 
+constexpr uint8_t TF_SINGLE = 1;   // big tile finished in place by k_accum_hot (one chunk)
+constexpr uint8_t TF_SPLIT = 2;    // big tile accumulated per half (split in every pending segment)
+
 struct Plan {
   uint32_t* tile_tot;      // [F]
   uint32_t* cold_tile;     // [F] cold item -> tile
-  uint32_t* hot_item;      // [hot items] big-tile chunk item -> tile | chunk << 15
-  uint32_t* hot_list;      // [F] multi-chunk tiles
-  uint32_t* header;        // [4] cold items, multi-chunk tiles, warm/hot items
+  uint32_t* hot_item;      // [hot items] big-tile chunk item -> tile | chunk << 15 (mixed halves)
+  uint2* split_item;       // [split items] {tile | half << 15, chunk} of split tiles
+  uint32_t* hot_list;      // [F] big tiles
+  uint8_t* tile_flags;     // [F] TF_*
+  uint32_t* header;        // [4] cold items, big tiles, mixed-half items, split items
 };
 
 struct Outputs {
@@ -81,36 +102,46 @@ struct Outputs {
 
 // ---- launchers (all enqueue on `st`) ----
 // hint: 2 hot tile ids (or ~0u) used only to merge LDS atomics
+// Count table: [G][F + COLS] (tile columns, then the half columns of split tiles).
 hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
-                        uint32_t* table, uint32_t* err, const uint32_t* hint, bool vec, hipStream_t st);
-hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* tile_tot, hipStream_t st);
-hipError_t launch_tilescan(const uint32_t* tile_tot, uint32_t F, uint32_t* tile_base, hipStream_t st);
+                        uint32_t* table, uint32_t* err, const uint32_t* hint, const uint32_t* split, bool vec,
+                        hipStream_t st);
+// Column prefixes over slabs (in place) and column totals coltot[F + COLS].
+hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* coltot, hipStream_t st);
+// Tile totals (split tiles: sum of their halves, written to coltot[t]) and tile_base[F+1].
+hipError_t launch_tilescan(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base, hipStream_t st);
+// Segment split info from the batch's split set and half-0 totals.
+hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st);
+// Single-level scatter (batches counted without split tiles).
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
                       int64_t* sumfix, bool vec, hipStream_t st);
 // Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
 // (super-tile -> tiles).  scratch1 holds n level-1 records.
-// Direct tiles: up to DIRECT_MAX tiles with the most records bypass level 2 --
-// k_bin1 writes their final records straight into the final layout.
-constexpr int DIRECT_MAX = 512;
-constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + direct tiles (<= 512)
+// Direct bins: the two halves of every split tile bypass level 2 -- k_bin1 writes
+// their records straight into the final layout.
+constexpr int DIRECT_MAX = SPLIT_MAX;
+constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + 2 x split tiles + the trash bin
 // k_bin1 LDS for a sub-chunk of ch slots: stage, cnt, oc, direct words + prefixes, hot slots, hot counters
 constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4; }
 constexpr size_t BIN1_SCRATCH_PAD = 16384 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
-constexpr int PLAN_WORDS = 8192;
-constexpr int PLAN_HINT = 2040;     // [2] hot-tile hints for the next batch's k_count
-constexpr int PLAN_DBITS = 2048;    // [1024] direct-tile bitmap (bit t of word t/32)
-constexpr int PLAN_DPRE = 3072;     // [1024] direct tiles before word w
-constexpr int PLAN_DLIST = 4096;    // [512] direct tile ids, ascending
-constexpr int PLAN_ND = 4608;       // number of direct tiles
-// Super-tile plan (level-2 items, direct tiles, hot keys).  A tile is direct when
-// its records >= max(thr_min, 2^k), k the smallest power keeping <= dmax tiles.
-hipError_t launch_stplan(uint32_t F, int G, const uint32_t* tile_tot, uint32_t* stplan, uint32_t thr_min,
-                         uint32_t dmax, hipStream_t st);
+constexpr int PLAN_HINT = 2040;     // [2] hot count-table columns: hints for the next batch's k_count
+constexpr int PLAN_DBITS = 2048;    // [1024] split-tile bitmap of this batch (bit t of word t/32)
+constexpr int PLAN_DPRE = 3072;     // [1024] split tiles before word w
+constexpr int PLAN_DLIST = 4096;    // [512] split tile ids, ascending
+constexpr int PLAN_ND = 4608;       // number of split tiles
+constexpr int PLAN_SPLIT = 8192;    // two split-set slots (this batch's, the next batch's)
+constexpr int PLAN_WORDS = PLAN_SPLIT + 2 * SPLIT_SLOT;
+// Super-tile plan (level-2 items, direct bins, hot keys) for this batch's split
+// set `cur`, and the next batch's split set `nxt`: the tiles with records >=
+// max(thr_min, 2^k), k the smallest power keeping <= dmax tiles.
+hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg, hipStream_t st);
+                       const uint32_t* coltot, uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg,
+                       hipStream_t st);
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
                        const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
                        hipStream_t st);
@@ -120,6 +151,8 @@ hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t ho
 hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st);
+hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t split_items, State state, Tables tb, uint32_t hot_chunk,
+                              hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
                              int reset, uint32_t hot_chunk, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external

@@ -23,9 +23,23 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
   __shared__ uint32_t lds_a[17];
   __shared__ uint32_t lds_b[17];
   __shared__ uint32_t lds_c[17];
+  __shared__ uint32_t lds_d[17];
   const uint32_t per = (F + 1023) / 1024;
   const uint32_t t0 = threadIdx.x * per;
-  uint32_t ci = 0, hi = 0, hot = 0;  // cold items, warm/hot items, multi-chunk tiles
+  // cold items, mixed-half chunk items, big tiles, split items
+  uint32_t ci = 0, hi = 0, hot = 0, si = 0;
+  // a big tile is accumulated per half when it is split in every pending segment:
+  // returns its half-0 records across the segments (or ~0u)
+  auto split_h0 = [&](uint32_t t) -> uint32_t {
+    if (segs.n == 0) return 0xFFFFFFFFu;
+    uint32_t h0 = 0;
+    for (int j = 0; j < segs.n; ++j) {
+      const uint16_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
+      if (m == NO_SPLIT) return 0xFFFFFFFFu;
+      h0 += segs.sinfo[j][SINFO_H0 + m];
+    }
+    return h0;
+  };
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t t = t0 + k;
     if (t >= F) break;
@@ -33,33 +47,51 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
     plan.tile_tot[t] = tot;
     if (tot > cold_limit) {
-      hi += (tot + hot_chunk - 1) / hot_chunk;
       hot += 1;
+      const uint32_t h0 = split_h0(t);
+      if (h0 != 0xFFFFFFFFu)
+        si += (h0 + hot_chunk - 1) / hot_chunk + (tot - h0 + hot_chunk - 1) / hot_chunk;
+      else
+        hi += (tot + hot_chunk - 1) / hot_chunk;
     } else if (final_mode || tot > 0) {
       ci += 1;
     }
   }
-  uint32_t tot_c, tot_h, tot_hot;
+  uint32_t tot_c, tot_h, tot_hot, tot_s;
   uint32_t ca = block_excl_scan<1024>(ci, lds_a, &tot_c);
   uint32_t ha = block_excl_scan<1024>(hi, lds_b, &tot_h);
   uint32_t xa = block_excl_scan<1024>(hot, lds_c, &tot_hot);
+  uint32_t sa = block_excl_scan<1024>(si, lds_d, &tot_s);
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t t = t0 + k;
     if (t >= F) break;
     const uint32_t tot = plan.tile_tot[t];
+    uint8_t flags = 0;
     if (tot > cold_limit) {
-      const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
-      for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
-      ha += nc;
+      const uint32_t h0 = split_h0(t);
+      if (h0 != 0xFFFFFFFFu) {
+        flags = TF_SPLIT;
+        for (uint32_t h = 0; h < 2; ++h) {
+          const uint32_t nh = ((h ? tot - h0 : h0) + hot_chunk - 1) / hot_chunk;
+          for (uint32_t c = 0; c < nh; ++c) plan.split_item[sa++] = make_uint2(t | (h << 15), c);
+        }
+      } else {
+        const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
+        for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
+        ha += nc;
+        if (tot <= hot_chunk) flags = TF_SINGLE;
+      }
       plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
       plan.cold_tile[ca++] = t;
     }
+    plan.tile_flags[t] = flags;
   }
   if (threadIdx.x == 0) {
     plan.header[0] = tot_c;
     plan.header[1] = tot_hot;
     plan.header[2] = tot_h;
+    plan.header[3] = tot_s;
   }
 }
 
@@ -67,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
 // clean ones start from zero.
 __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t hot_chunk) {
   const uint32_t t = plan.hot_list[blockIdx.x];
-  if (st.dirty[t] || plan.tile_tot[t] <= hot_chunk) return;  // single-chunk tiles emit in place
+  if (st.dirty[t] || (plan.tile_flags[t] & TF_SINGLE)) return;  // single-chunk tiles emit in place
   const uint32_t s0 = t * TILE;
   const uint32_t s1 = min(st.S, s0 + TILE);
   uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
@@ -96,14 +128,21 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   uint32_t* srow = st.counts + (size_t)s * ROW;
   uint32_t g[9];
   if (!dirty) {
-    // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are padding)
+    // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are
+    // padding); even output rows are 16-B aligned and take one 16-B store per group
+    const bool al16 = (oi & 1u) == 0u;
 #pragma unroll 2
     for (int k = 0; k < 8; ++k) {
       const int q = lane + 64 * k;
       if (q < NB4) {
         const int b0 = 4 * q;
         const uint4 v = lds.get4(b0);
-        if (orow && !(g_dbg & 0x200)) store4_1798(orow, b0, v);
+        if (orow && !(g_dbg & 0x200)) {
+          if (al16 && b0 != 1796)
+            *reinterpret_cast<uint4*>(orow + b0) = v;
+          else
+            store4_1798(orow, b0, v);
+        }
         if (keep) store4_state(srow, b0, v);
       }
     }
@@ -345,6 +384,7 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   const uint32_t t = hx & 0x7FFFu;
   const uint32_t sub = hx >> 15;
   const uint32_t tot = plan.tile_tot[t];
+  (void)hot_chunk;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
@@ -394,13 +434,85 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   // not have read it yet.
 }
 
+// Split big tiles (split in every pending segment): item = (tile, half, chunk of
+// hot_chunk records of that half).  A segment holds the tile's half-0 records at
+// [tbase, tbase + h0) and its half-1 records after them, so each item reads one
+// contiguous range per segment, with no filtering.  u32 LDS bins for the half's
+// 16 series, lane-private value sums, flushed with global atomics (k_hot_init
+// cleared the rows; k_hot_finish summarizes them).
+__global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, uint32_t hot_chunk) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint2 it = plan.split_item[blockIdx.x];
+  const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  uint32_t* hist = smem;                                                              // [16][1800]
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] value sums
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + 16 * 64);                              // [LUT2_N]
+  {
+    uint4* q = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
+  }
+  __syncthreads();
+  const uint64_t vlo = (uint64_t)it.y * hot_chunk, vhi = vlo + hot_chunk;
+  uint64_t vbase = 0;
+  for (int j = 0; j < segs.n; ++j) {
+    const uint32_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
+    const uint32_t h0 = segs.sinfo[j][SINFO_H0 + m];
+    const uint32_t ta = segs.tbase[j][t], te = segs.tbase[j][t + 1];
+    const uint32_t a0 = half ? ta + h0 : ta;
+    const uint64_t len = half ? te - ta - h0 : h0;
+    const uint64_t lo = vlo > vbase ? vlo : vbase;
+    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+    const uint64_t skip = lo - vbase;
+    vbase += len;
+    if (lo >= hi) continue;
+    const uint32_t a = a0 + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
+    const uint32_t* __restrict__ r = segs.recs[j];
+    auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
+    const uint32_t a4 = a & ~3u;
+    uint32_t g = a4 + 4u * threadIdx.x;
+    uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
+    for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
+      const uint4 x0 = n0, x1 = n1;
+      n0 = ld(g + 8u * WG);
+      n1 = ld(g + 12u * WG);
+      uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+        if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+      }
+      count_batch<8>(
+          x, lut2, [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
+          [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
+    }
+  }
+  __syncthreads();
+  const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
+  const uint32_t s = t * TILE + 16 * half + w;
+  if (s < st.S) {
+    uint32_t* grow = st.counts + (size_t)s * ROW;
+    const uint32_t* hrow = hist + w * HROW;
+    for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+      const int b = b0 + lane;
+      const uint32_t v = b < NB ? hrow[b] : 0u;
+      if (__ballot(v != 0u)) {
+        if (v) atomicAdd(&grow[b], v);
+      }
+    }
+    if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
+  }
+}
+
 // k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
 // write outputs, update state/dirty.
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
                                                    int reset, uint32_t hot_chunk) {
   const uint32_t t = plan.hot_list[blockIdx.x >> 1];
   const uint32_t half = blockIdx.x & 1u;
-  if (plan.tile_tot[t] <= hot_chunk) {  // emitted by k_accum_hot
+  if (plan.tile_flags[t] & TF_SINGLE) {  // emitted by k_accum_hot
     if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
     return;
   }
@@ -482,6 +594,8 @@ hipError_t set_snapshot_debug(int dbg) { return hipMemcpyToSymbol(HIP_SYMBOL(g_d
 hipError_t set_snapshot_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
+  if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
 }
 
@@ -513,6 +627,13 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
     return hipGetLastError();
   }
   return hipSuccess;
+}
+
+hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t split_items, State state, Tables tb, uint32_t hot_chunk,
+                              hipStream_t st) {
+  if (split_items == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_accum_split, dim3(split_items), dim3(WG), ACC_SPLIT_LDS, st, segs, plan, state, tb, hot_chunk);
+  return hipGetLastError();
 }
 
 hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
