@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--bin-mode", type=int, default=0)
     p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..512)")
     p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
+    p.add_argument("--split-min", type=int, default=None, help="engine param: min records of a split tile")
     p.add_argument("--cpu-sample", type=int, default=20_000_000, help="samples in the CPU baseline sample (0: skip)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_latest.json"))
@@ -178,6 +179,8 @@ def main():
         eng.set_param(N_.PARAM_DIRECT_MAX, args.direct_max)
     if args.direct_div is not None:
         eng.set_param(N_.PARAM_DIRECT_DIV, args.direct_div)
+    if args.split_min is not None:
+        eng.set_param(N_.PARAM_SPLIT_MIN, args.split_min)
     summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
     counts = torch.empty((S, N_.NBUCKETS), dtype=torch.int32, device=dev)
 

@@ -33,6 +33,7 @@ PARAM_MAX_SEGMENTS = 4
 PARAM_BIN_MODE = 5
 PARAM_DIRECT_MAX = 6
 PARAM_DIRECT_DIV = 7
+PARAM_SPLIT_MIN = 8
 
 K_COUNT, K_SCAN, K_BIN, K_ACCUM, K_HOT, K_COPY, K_BIN2 = range(7)
 KERNEL_NAMES = ("count", "scan", "bin1", "accum", "hot", "copy", "bin2")

@@ -202,6 +202,7 @@ struct l5dh_ctx {
   uint32_t direct_max = DIRECT_MAX;  // tiles k_bin1 may write in final form (0: none)
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
+  uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
@@ -463,18 +464,19 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       KTimer kt(c, L5DH_K_SCAN);
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
       HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
-                              (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->stream));
+                              (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
+                              c->stream));
       c->split_cur ^= 1;
     }
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
-                            c->d_tile_tot, static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
+                            c->d_tile_tot, cur, static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
                             c->dbg, c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
-    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, tables(c),
-                          c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->stream));
+    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, c->d_tile_tot,
+                          cur, tables(c), c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->dbg, c->stream));
   } else {
     KTimer kt(c, L5DH_K_BIN);
     HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
@@ -839,12 +841,16 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->bin_mode = (int)v;
       return 0;
     case L5DH_PARAM_DIRECT_MAX:
-      if (v < 0 || v > DIRECT_MAX) return fail(c, -EINVAL, "direct tiles must be in [0, 512]");
+      if (v < 0 || v > DIRECT_MAX) return fail(c, -EINVAL, "direct tiles must be in [0, 255]");
       c->direct_max = (uint32_t)v;
       return 0;
     case L5DH_PARAM_DIRECT_DIV:
       if (v < 1 || v > 65536) return fail(c, -EINVAL, "direct divisor must be in [1, 65536]");
       c->direct_div = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_SPLIT_MIN:
+      if (v < 1 || v > 0xFFFFFFFFll) return fail(c, -EINVAL, "split minimum must be in [1, 2^32)");
+      c->split_min = (uint32_t)v;
       return 0;
     default:
       return fail(c, -EINVAL, "unknown parameter");

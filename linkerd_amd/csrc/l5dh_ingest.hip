@@ -22,9 +22,7 @@ constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
-constexpr int B2_NT = 256;
 constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
-constexpr int CH2 = 4096;            // k_bin2 sub-chunk (LDS counting sort by tile)
 
 // ------------------------------------------------------------------------
 // Count key of a valid sample: its tile, or for a split tile the column of its
@@ -261,7 +259,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base, Tables tb,
                                                 const uint32_t* __restrict__ plan, const uint32_t* __restrict__ coltot,
-                                                uint32_t* __restrict__ out1, uint32_t* __restrict__ records,
+                                                const uint32_t* __restrict__ split, uint32_t* __restrict__ out1, uint32_t* __restrict__ records,
                                                 int64_t* __restrict__ sumfix, int vec, int dbg) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
@@ -288,18 +286,27 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
     cnt[b] = 0;
   }
   for (uint32_t i = threadIdx.x; i < (NHOT + 1) * 64; i += NT) hcnt[i] = 0;
-  for (uint32_t j = threadIdx.x; j < FS; j += NT) {
-    const uint32_t t0 = j * ST_TILES;
-    const uint32_t t1 = min(F, t0 + ST_TILES);
-    uint32_t acc = tile_base[t0];
-    for (uint32_t t = t0; t < t1; ++t)
-      if (!((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) acc += prow[t];
-    oc[j] = make_uint2(0u, acc);
+  // super-tile cursors: level-1 records of this slab before super-tile j; one
+  // wave per super-tile, a lane per tile (independent, coalesced loads)
+  for (uint32_t t = threadIdx.x; t < FS * ST_TILES; t += NT) {
+    uint32_t v = 0;
+    if (t < F && !((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) {  // direct tiles have no level-1 records
+      const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
+      const uint32_t bit = 1u << (t & 31u);
+      if (wd & bit) {  // split: its count is in the two half columns
+        const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
+        v = prow[F + 2 * si] + prow[F + 2 * si + 1];
+      } else {
+        v = prow[t];
+      }
+    }
+    v = wave_sum(v);
+    if (lane == 0) oc[t >> 6] = make_uint2(0u, tile_base[t] + v);
   }
-  for (uint32_t h = threadIdx.x; h < 2 * ND; h += NT) {  // split tile h/2: half 0 from its start, half 1 after it
-    const uint32_t si = h >> 1;
-    const uint32_t t = plan[PLAN_DLIST + si];
-    const uint32_t at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + h];
+  for (uint32_t h = threadIdx.x; h < 2 * ND; h += NT) {  // direct tile h/2: half 0 from its start, half 1 after it
+    const uint32_t si = plan[PLAN_DSI + (h >> 1)];
+    const uint32_t t = plan[PLAN_DLIST + (h >> 1)];
+    const uint32_t at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + 2 * si + (h & 1u)];
     oc[FS + h] = make_uint2(0u, at | 0x80000000u);
   }
   if (threadIdx.x == 0) oc[TB] = make_uint2(0u, trash);
@@ -455,41 +462,51 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 //   plan[PLAN_HINT..+1]  hot count columns for the next batch's k_count
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
                                                  uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
-                                                 uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax) {
+                                                 uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax,
+                                                 uint32_t split_min) {
   __shared__ uint32_t lds[17];
   __shared__ unsigned long long best[16];
-  __shared__ uint32_t lhist[33];
-  __shared__ uint32_t sthr;
+  __shared__ uint32_t lhd[33], lhs[33];
+  __shared__ uint32_t sthr[2];
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t j = threadIdx.x;
-  // next split set: smallest power of two (>= thr_min) selecting <= dmax tiles
-  if (j < 33) lhist[j] = 0;
+  const uint32_t NS = cur[0];
+  if (j < 33) lhd[j] = lhs[j] = 0;
   __syncthreads();
+  // direct tiles: split tiles of this batch with >= max(thr_min, 2^k) records;
+  // next split set: tiles with >= max(split_min, 2^k) records
   if (dmax > 0)
-    for (uint32_t t = j; t < F; t += 1024) {
-      const uint32_t v = coltot[t];
-      if (v >= thr_min && v > 0) atomicAdd(&lhist[31 - __clz((int)v)], 1u);
+    for (uint32_t si = j; si < NS; si += 1024) {
+      const uint32_t v = coltot[cur[SPLIT_LIST + si]];
+      if (v >= thr_min && v > 0) atomicAdd(&lhd[31 - __clz((int)v)], 1u);
     }
+  for (uint32_t t = j; t < F; t += 1024) {
+    const uint32_t v = coltot[t];
+    if (v >= split_min && v > 0) atomicAdd(&lhs[31 - __clz((int)v)], 1u);
+  }
   __syncthreads();
-  if (j == 0) {
-    // cum_k = tiles with v >= thr_min and floor(log2 v) >= k (non-increasing in k):
-    // the smallest k with cum_k <= dmax gives thr = max(thr_min, 2^k)
+  if (j < 2) {
+    // cum_k = tiles with floor(log2 v) >= k (non-increasing in k): the smallest k
+    // with cum_k <= cap gives thr = max(lo, 2^k)
+    const uint32_t* lh = j ? lhs : lhd;
+    const uint32_t cap = j ? (uint32_t)SPLIT_MAX : dmax;
+    const uint32_t lo = max(j ? split_min : thr_min, 1u);
     uint32_t thr = NOKEY;
-    if (dmax > 0) {
+    if (cap > 0) {
       uint32_t cum = 0;
       int kbest = 32;
       for (int k = 31; k >= 0; --k) {
-        cum += lhist[k];
-        if (cum > dmax) break;
+        cum += lh[k];
+        if (cum > cap) break;
         kbest = k;
       }
-      if (kbest < 32) thr = max(max(thr_min, 1u), 1u << kbest);
+      if (kbest < 32) thr = max(lo, 1u << kbest);
     }
-    sthr = thr;
+    sthr[j] = thr;
   }
   __syncthreads();
-  const uint32_t thr = sthr;
-  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nn = 0, n0 = 0, n1 = 0;
+  const uint32_t thr_d = sthr[0], thr_s = sthr[1];
+  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nn = 0, ndt = 0, n0 = 0, n1 = 0, d0 = 0, d1 = 0;
   uint32_t c0 = 0, c1 = 0;  // this batch's split words of the super-tile
   uint64_t ctot = 0, tot = 0;
   unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile): this thread's two biggest tiles
@@ -497,7 +514,7 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     c0 = cur[SPLIT_BITS + 2 * j];
     c1 = 2 * j + 1 < 1024 ? cur[SPLIT_BITS + 2 * j + 1] : 0u;
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest non-split tiles of this super-tile
+    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest level-1 tiles of this super-tile
     uint32_t a0 = 0, a1 = 0, k0 = 0xFF, k1 = 0xFF;  // two biggest tiles
     for (uint32_t t = j * ST_TILES; t < t1; ++t) {
       const uint32_t v = coltot[t];
@@ -505,20 +522,25 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       tot += v;
       if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
       else if (v > a1) { a1 = v; k1 = tl; }
-      if (v >= thr) {
+      if (v >= thr_s) {
         if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
       }
-      if (((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u) continue;  // split now: no level-1 records
+      const bool split = ((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u;
+      if (split && v >= thr_d) {  // direct: no level-1 records
+        if (tl < 32) d0 |= 1u << tl; else d1 |= 1u << (tl - 32);
+        continue;
+      }
       ctot += v;
       if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
       else if (v > b1) { b1 = v; i1 = tl; }
     }
     nn = (uint32_t)(__popc(n0) + __popc(n1));
+    ndt = (uint32_t)(__popc(d0) + __popc(d1));
     tkA = k0 != 0xFF ? (((unsigned long long)a0 << 16) | (j * ST_TILES + k0)) : 0ull;
     tkB = k1 != 0xFF ? (((unsigned long long)a1 << 16) | (j * ST_TILES + k1)) : 0ull;
     if ((uint64_t)b0 * 8 < ctot || b0 == 0) i0 = 0xFF;
     if ((uint64_t)b1 * 8 < ctot || b1 == 0) i1 = 0xFF;
-    hot = i0 | (i1 << 8);
+    hot = (i0 == 0xFF ? 0xFFu : 2 * i0) | ((i1 == 0xFF ? 0xFFu : 2 * i1) << 8);  // k_bin2 keys (half 0)
     if (ctot > 0) {
       uint32_t want = (uint32_t)((ctot + B2_ITEM - 1) / B2_ITEM);
       want = max(1u, min(want, (uint32_t)G));
@@ -528,9 +550,10 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       gsz = (uint32_t)G;
     }
   }
-  uint32_t total, nnt;
+  uint32_t total, nnt, ndtot;
   const uint32_t e = block_excl_scan<1024>(nb, lds, &total);
   const uint32_t ne = block_excl_scan<1024>(nn, lds, &nnt);
+  const uint32_t de = block_excl_scan<1024>(ndt, lds, &ndtot);
   // this thread's NHOT biggest k_bin1 bins, descending: (records << 11 | bin)
   unsigned long long bk[NHOT] = {};
   auto push = [&](unsigned long long k) {
@@ -546,23 +569,26 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     plan[j] = e;
     plan[FS + 1 + j] = gsz;
     plan[2 * FS + 1 + j] = hot;
-    // this batch's split tiles (copied for k_bin1 / k_bin2) and their half bins
-    plan[PLAN_DBITS + 2 * j] = c0;
-    plan[PLAN_DPRE + 2 * j] = cur[SPLIT_PRE + 2 * j];
+    // this batch's direct tiles, their split index and half bins
+    plan[PLAN_DBITS + 2 * j] = d0;
+    plan[PLAN_DPRE + 2 * j] = de;
     if (2 * j + 1 < 1024) {
-      plan[PLAN_DBITS + 2 * j + 1] = c1;
-      plan[PLAN_DPRE + 2 * j + 1] = cur[SPLIT_PRE + 2 * j + 1];
+      plan[PLAN_DBITS + 2 * j + 1] = d1;
+      plan[PLAN_DPRE + 2 * j + 1] = de + (uint32_t)__popc(d0);
     }
-    uint32_t si = cur[SPLIT_PRE + 2 * j];
+    uint32_t di = de;
     for (int q = 0; q < 2; ++q) {
-      uint32_t w = q ? c1 : c0;
+      uint32_t w = q ? d1 : d0;
+      const uint32_t cw = q ? c1 : c0;
       while (w) {
-        const uint32_t tl = (uint32_t)(__ffs((int)w) - 1) + 32u * q;
+        const uint32_t b = (uint32_t)(__ffs((int)w) - 1);
         w &= w - 1u;
-        plan[PLAN_DLIST + si] = j * ST_TILES + tl;
-        push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * si));
-        push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * si + 1));
-        ++si;
+        const uint32_t si = cur[SPLIT_PRE + 2 * j + q] + (uint32_t)__popc(cw & ((1u << b) - 1u));
+        plan[PLAN_DLIST + di] = j * ST_TILES + 32u * q + b;
+        plan[PLAN_DSI + di] = si;
+        push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * di));
+        push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * di + 1));
+        ++di;
       }
     }
     if (ctot) push((ctot << 11) | j);
@@ -585,7 +611,7 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   }
   if (threadIdx.x == 0) {
     plan[FS] = total;
-    plan[PLAN_ND] = cur[0];
+    plan[PLAN_ND] = ndtot;
     nxt[0] = nnt;
   }
   // grand total, the hot bins and the two biggest tiles (block reductions)
@@ -648,20 +674,28 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
 }
 
 // Level 2.  Item = (super-tile j, slab range [g0, g1)).  Its level-1 records are
-// one contiguous range; tile t's records of that range go, in any order, to
-// [tile_base[t] + pre[g0][t], ...) -- exactly where the per-(slab, tile)
-// segments g0..g1-1 of the final layout lie.
+// one contiguous range; the records of tile t (of half h of t, for a split tile)
+// in that range go, in any order, to [tile_base[t] (+ half-0 total) + pre[g0][col],
+// ...) -- exactly where the per-(slab, tile) segments g0..g1-1 of the final
+// layout lie.  Keys: 2 x tile-in-ST + half (half 0 for an unsplit tile).
+constexpr int B2_KEYS = 2 * ST_TILES;
+constexpr size_t bin2_lds(int ch) { return (size_t)ch * 8 + 3 * B2_KEYS * 4 + 16; }
+template <int CH2, int B2_NT>
 __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out1, uint32_t F, int G,
                                                 const uint32_t* __restrict__ pre,
                                                 const uint32_t* __restrict__ tile_base,
+                                                const uint32_t* __restrict__ coltot,
+                                                const uint32_t* __restrict__ split,
                                                 const uint32_t* __restrict__ plan, Tables tb,
                                                 uint32_t* __restrict__ records) {
-  __shared__ uint32_t cur[ST_TILES];      // global write position of each tile
-  __shared__ uint32_t cnt[ST_TILES];      // records of each tile in this sub-chunk
-  __shared__ uint32_t off[ST_TILES];      // their exclusive offsets in stage
-  __shared__ uint2 stage[CH2];            // sub-chunk sorted by tile: {record, global index - stage index}
-  __shared__ uint32_t seg[2];
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint2* stage = reinterpret_cast<uint2*>(smem);  // [CH2] sub-chunk sorted by key: {record, global index - stage index}
+  uint32_t* cur = smem + 2 * CH2;                 // [B2_KEYS] global write position of each key
+  uint32_t* cnt = cur + B2_KEYS;                  // [B2_KEYS] records of each key in this sub-chunk
+  uint32_t* off = cnt + B2_KEYS;                  // [B2_KEYS] their exclusive offsets in stage
+  uint32_t* seg = off + B2_KEYS;                  // [2]
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t C = F + COLS;
   const uint32_t item = blockIdx.x;
   if (item >= plan[FS]) return;
   uint32_t lo = 0, hi = FS;  // last j with plan[j] <= item
@@ -679,18 +713,38 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t hk[2] = {hot0, hot1};
   const uint32_t t0 = j * ST_TILES;
   const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
+  // split (and not direct) tiles of the super-tile: records keyed by half
+  const uint32_t sw0 = split[SPLIT_BITS + 2 * j] & ~plan[PLAN_DBITS + 2 * j];
+  const uint32_t sw1 = 2 * j + 1 < 1024 ? split[SPLIT_BITS + 2 * j + 1] & ~plan[PLAN_DBITS + 2 * j + 1] : 0u;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    uint32_t p0 = 0, p1 = 0;
+    uint32_t q0 = 0, q1 = 0, r0 = 0, r1 = 0;  // keys 2 lane, 2 lane + 1: pre[g0], pre[g1]
     if ((uint32_t)lane < nt) {
       const uint32_t t = t0 + lane;
-      const bool direct = (plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u;
-      p0 = pre[(size_t)g0 * (F + COLS) + t];
-      cur[lane] = tile_base[t] + p0;
-      p1 = g1 < G ? pre[(size_t)g1 * (F + COLS) + t] : (tile_base[t + 1] - tile_base[t]);
-      if (direct) p0 = p1 = 0;  // its records never reach level 1
+      const uint32_t bit = 1u << (t & 31u);
+      const bool direct = plan[PLAN_DBITS + (t >> 5)] & bit;
+      const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
+      const uint32_t tb0 = tile_base[t];
+      if (direct) {  // its records never reach level 1
+        cur[2 * lane] = cur[2 * lane + 1] = tb0;
+      } else if (wd & bit) {
+        const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
+        const uint32_t c0 = F + 2 * si;
+        q0 = pre[(size_t)g0 * C + c0];
+        q1 = pre[(size_t)g0 * C + c0 + 1];
+        r0 = g1 < G ? pre[(size_t)g1 * C + c0] : coltot[c0];
+        r1 = g1 < G ? pre[(size_t)g1 * C + c0 + 1] : coltot[c0 + 1];
+        cur[2 * lane] = tb0 + q0;
+        cur[2 * lane + 1] = tb0 + coltot[c0] + q1;
+      } else {
+        q0 = pre[(size_t)g0 * C + t];
+        r0 = g1 < G ? pre[(size_t)g1 * C + t] : (tile_base[t + 1] - tb0);
+        cur[2 * lane] = tb0 + q0;
+        cur[2 * lane + 1] = 0;
+      }
     }
-    cnt[lane] = 0;
+    cnt[2 * lane] = cnt[2 * lane + 1] = 0;
+    uint32_t p0 = q0 + q1, p1 = r0 + r1;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
       p0 += __shfl_xor(p0, d, 64);
@@ -704,7 +758,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   __syncthreads();
   const uint32_t A = seg[0], B = seg[1];
   const uint32_t A16 = A & ~3u;  // 16-B aligned start; lanes below A are masked off
-  constexpr int PT = CH2 / B2_NT;  // 16 records per thread: 4 x uint4
+  constexpr int PT = CH2 / B2_NT;  // records per thread (groups of 4)
   uint4 xn[PT / 4];                 // next sub-chunk, prefetched while this one is sorted and written
 #pragma unroll
   for (int k = 0; k < PT / 4; ++k) {
@@ -712,7 +766,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     xn[k] = base < B ? *reinterpret_cast<const uint4*>(out1 + base) : make_uint4(0u, 0u, 0u, 0u);
   }
   for (uint32_t c0 = A16; c0 < B; c0 += CH2) {
-    uint32_t rec[PT], tlv[PT], rank[PT];
+    uint32_t rec[PT], kv[PT], rank[PT];
     uint4 xc[PT / 4];
 #pragma unroll
     for (int k = 0; k < PT / 4; ++k) {
@@ -731,32 +785,29 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
         const bool valid = idx >= A && idx < B;
         const uint32_t r = xv[e];
         const uint32_t tl = r >> 26;
-        rec[4 * k + e] = r;  // records pass through unchanged (tile order is all that changes)
-        tlv[4 * k + e] = valid ? tl : 0xFFFFFFFFu;
+        const uint32_t sp = ((tl < 32 ? sw0 : sw1) >> (tl & 31u)) & 1u;
+        rec[4 * k + e] = r;  // records pass through unchanged (key order is all that changes)
+        kv[4 * k + e] = valid ? 2u * tl + (sp & (r >> 25)) : 0xFFFFFFFFu;
       }
     }
-    hot_rank_batch<2, PT>(cnt, tlv, hk, rank);
+    hot_rank_batch<2, PT>(cnt, kv, hk, rank);
     __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 64 tile counts (one wave)
-      const uint32_t v = cnt[threadIdx.x];
-      uint32_t x = v;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if ((int)threadIdx.x >= d) x += y;
-      }
-      off[threadIdx.x] = x - v;
+    if (threadIdx.x < 64) {  // exclusive scan of the 128 key counts (one wave, two per lane)
+      const uint32_t a = cnt[2 * threadIdx.x], b = cnt[2 * threadIdx.x + 1];
+      const uint32_t x = wave_incl_scan32(a + b) - (a + b);
+      off[2 * threadIdx.x] = x;
+      off[2 * threadIdx.x + 1] = x + a;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      if (tlv[k] != 0xFFFFFFFFu) {
-        const uint32_t o = off[tlv[k]];
+      if (kv[k] != 0xFFFFFFFFu) {
+        const uint32_t o = off[kv[k]];
         const uint32_t pos = o + rank[k];
-        stage[pos] = make_uint2(rec[k], cur[tlv[k]] - o);
+        stage[pos] = make_uint2(rec[k], cur[kv[k]] - o);
       }
     }
-    const uint32_t total = off[ST_TILES - 1] + cnt[ST_TILES - 1];
+    const uint32_t total = off[B2_KEYS - 1] + cnt[B2_KEYS - 1];
     __syncthreads();
     {
       uint2 ev[PT];
@@ -768,7 +819,7 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
         if (i < total) records[ev[k].y + i] = ev[k].x;
       }
     }
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < B2_KEYS) {
       cur[threadIdx.x] += cnt[threadIdx.x];
       cnt[threadIdx.x] = 0;
     }
@@ -789,6 +840,12 @@ hipError_t set_ingest_attributes() {
     return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bin1_lds(16384))))
+    return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin2<8192, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bin2_lds(8192))))
+    return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin2<16384, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bin2_lds(16384))))
     return e;
 
 
@@ -828,36 +885,43 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
 }
 
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
-                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, hipStream_t st) {
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, hipStream_t st) {
   const uint32_t FS = (F + 63) / 64;
-  const uint32_t cap = std::min<uint32_t>((uint32_t)SPLIT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
-  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap));
+  const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
+  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap),
+                     split_min);
   return hipGetLastError();
 }
 
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       const uint32_t* coltot, uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg,
-                       hipStream_t st) {
+                       const uint32_t* coltot, const uint32_t* split, uint32_t* scratch1, uint32_t* records,
+                       int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
   // sub-chunk size x workgroup: (16384 slots, 1024 threads, 1 workgroup/CU) by
   // default -- longer runs per bin beat the second workgroup's overlap (measured);
   // L5DH_DBG bit 20 selects (6144, 512, 2 workgroups/CU)
   if ((dbg >> 20) & 1)
     hipLaunchKernelGGL((k_bin1<6144, 512, 4>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
-                       pre, tile_base, tb, stplan, coltot, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+                       pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   else
     hipLaunchKernelGGL((k_bin1<16384, 1024, 4>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
-                       F, pre, tile_base, tb, stplan, coltot, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+                       F, pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
 
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
-                       const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
-                       hipStream_t st) {
+                       const uint32_t* tile_base, const uint32_t* coltot, const uint32_t* split, Tables tb,
+                       const uint32_t* stplan, uint32_t* records, int dbg, hipStream_t st) {
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const size_t max_items = n / B2_ITEM + FS + 1;  // sum_j ceil(tot_j / B2_ITEM)
-  hipLaunchKernelGGL(k_bin2, dim3((unsigned)max_items), dim3(B2_NT), 0, st, scratch1, F, G, pre, tile_base, stplan,
-                     tb, records);
+  // sub-chunk x workgroup: (8192, 512) by default (measured: longer runs per key
+  // than (4096, 256)); L5DH_DBG bit 21: (16384, 1024)
+  if ((dbg >> 21) & 1)
+    hipLaunchKernelGGL((k_bin2<16384, 1024>), dim3((unsigned)max_items), dim3(1024), bin2_lds(16384), st, scratch1, F,
+                       G, pre, tile_base, coltot, split, stplan, tb, records);
+  else
+    hipLaunchKernelGGL((k_bin2<8192, 512>), dim3((unsigned)max_items), dim3(512), bin2_lds(8192), st, scratch1, F, G,
+                       pre, tile_base, coltot, split, stplan, tb, records);
   return hipGetLastError();
 }
 

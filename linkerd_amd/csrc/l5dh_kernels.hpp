@@ -46,17 +46,17 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
   const uint2* lut2;       // [LUT2_N] {o1 | o2 << 16, b0 | p << 16} (bucket_lut2)
 };
 
-// Split tiles: the hottest tiles of the previous batch (<= SPLIT_MAX) are counted,
+// Split tiles: the big tiles of the previous batch (<= SPLIT_MAX) are counted,
 // binned and laid out per half-tile (series 0-15 | 16-31): a split tile's region
 // holds its half-0 records first, then its half-1 records, so the big-tile
 // accumulation reads each half as one contiguous range.
-constexpr int SPLIT_MAX = 255;
+constexpr int SPLIT_MAX = 2040;
 constexpr int COLS = 2 * SPLIT_MAX;   // count-table columns past F: the half counters of split tiles
 // Split-set slot (SPLIT_SLOT u32): [0] NS | [1 + s] tile id (ascending) | bitmap | word prefixes
-constexpr int SPLIT_LIST = 1, SPLIT_BITS = 256, SPLIT_PRE = 1280, SPLIT_SLOT = 2304;
-// Per-segment split info (SINFO_WORDS(F) u32): [0] NS | [1 + s] tile | [256 + s] half-0 records
-// | u16 map tile -> s (0xFFFF: not split) from word 512
-constexpr int SINFO_H0 = 256, SINFO_MAP = 512;
+constexpr int SPLIT_LIST = 1, SPLIT_BITS = 2048, SPLIT_PRE = 3072, SPLIT_SLOT = 4096;
+// Per-segment split info (SINFO_WORDS(F) u32): [0] NS | [1 + s] tile | [2048 + s] half-0 records
+// | u16 map tile -> s (0xFFFF: not split) from word 4096
+constexpr int SINFO_H0 = 2048, SINFO_MAP = 4096;
 constexpr size_t sinfo_words(uint32_t F) { return SINFO_MAP + (F + 1) / 2 + 1; }
 constexpr uint16_t NO_SPLIT = 0xFFFF;
 
@@ -118,33 +118,35 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
                       int64_t* sumfix, bool vec, hipStream_t st);
 // Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
 // (super-tile -> tiles).  scratch1 holds n level-1 records.
-// Direct bins: the two halves of every split tile bypass level 2 -- k_bin1 writes
-// their records straight into the final layout.
-constexpr int DIRECT_MAX = SPLIT_MAX;
-constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + 2 x split tiles + the trash bin
+// Direct tiles (a subset of the split tiles, <= DIRECT_MAX): the two halves of each
+// bypass level 2 -- k_bin1 writes their records straight into the final layout.
+constexpr int DIRECT_MAX = 255;
+constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + 2 x direct tiles + the trash bin
 // k_bin1 LDS for a sub-chunk of ch slots: stage, cnt, oc, direct words + prefixes, hot slots, hot counters
 constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4; }
 constexpr size_t BIN1_SCRATCH_PAD = 16384 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
 constexpr int PLAN_HINT = 2040;     // [2] hot count-table columns: hints for the next batch's k_count
-constexpr int PLAN_DBITS = 2048;    // [1024] split-tile bitmap of this batch (bit t of word t/32)
-constexpr int PLAN_DPRE = 3072;     // [1024] split tiles before word w
-constexpr int PLAN_DLIST = 4096;    // [512] split tile ids, ascending
-constexpr int PLAN_ND = 4608;       // number of split tiles
+constexpr int PLAN_DBITS = 2048;    // [1024] direct-tile bitmap of this batch (bit t of word t/32)
+constexpr int PLAN_DPRE = 3072;     // [1024] direct tiles before word w
+constexpr int PLAN_DLIST = 4096;    // [256] direct tile ids, ascending
+constexpr int PLAN_DSI = 4352;      // [256] their split index
+constexpr int PLAN_ND = 4608;       // number of direct tiles
 constexpr int PLAN_SPLIT = 8192;    // two split-set slots (this batch's, the next batch's)
 constexpr int PLAN_WORDS = PLAN_SPLIT + 2 * SPLIT_SLOT;
 // Super-tile plan (level-2 items, direct bins, hot keys) for this batch's split
-// set `cur`, and the next batch's split set `nxt`: the tiles with records >=
-// max(thr_min, 2^k), k the smallest power keeping <= dmax tiles.
+// set `cur`: its direct tiles are the split tiles with records >= max(thr_min,
+// 2^k), k the smallest power keeping <= dmax tiles.  The next batch's split set
+// `nxt`: the tiles with records >= max(split_min, 2^k) (<= SPLIT_MAX tiles).
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
-                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, hipStream_t st);
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       const uint32_t* coltot, uint32_t* scratch1, uint32_t* records, int64_t* sumfix, bool vec, int dbg,
-                       hipStream_t st);
+                       const uint32_t* coltot, const uint32_t* split, uint32_t* scratch1, uint32_t* records,
+                       int64_t* sumfix, bool vec, int dbg, hipStream_t st);
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
-                       const uint32_t* tile_base, Tables tb, const uint32_t* stplan, uint32_t* records,
-                       hipStream_t st);
+                       const uint32_t* tile_base, const uint32_t* coltot, const uint32_t* split, Tables tb,
+                       const uint32_t* stplan, uint32_t* records, int dbg, hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
                        hipStream_t st);
 hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st);

@@ -145,6 +145,43 @@ def test_hot_tile_split_path(oracle, bin_mode):
     _assert_summaries_equal(got, o.snapshot(reset=False)[:40], "hot fold")
 
 
+@pytest.mark.parametrize("direct_max", [0, 2, 255])
+def test_split_tiles_across_batches(oracle, direct_max):
+    """Split tiles: the previous batch's big tiles are counted and laid out per
+    half-tile (direct ones by k_bin1, the rest through k_bin2).  Batches with
+    different hot tiles leave a tile split in some pending segments only (mixed
+    items) and in all of them (split items)."""
+    rng = np.random.default_rng(21 + direct_max)
+    S = 4000
+    eng = _engine(S, 2)
+    eng.set_param(N.PARAM_COLD_LIMIT, 500)
+    eng.set_param(N.PARAM_HOT_CHUNK, 5000)
+    eng.set_param(N.PARAM_MAX_SEGMENTS, 3)
+    eng.set_param(N.PARAM_DIRECT_MAX, direct_max)
+    eng.set_param(N.PARAM_SPLIT_MIN, 1000)
+    o = oracle.OracleHistograms(S)
+
+    def batch(hot_lo, hot_hi, n_hot, n_cold):
+        series = np.concatenate([rng.integers(hot_lo, hot_hi, n_hot), rng.integers(0, S, n_cold)]).astype(np.uint32)
+        rng.shuffle(series)
+        vals = np.exp(2 + 1.5 * rng.standard_normal(series.size)).astype(np.float32)
+        vals[::89] = rng.choice(EDGE_VALUES, size=vals[::89].size)
+        return series, vals
+
+    plan = [[(0, 64, 30_000, 5_000)], [(32, 100, 40_000, 8_000), (0, 20, 12_000, 1_000)],
+            [(0, 64, 25_000, 3_000), (0, 64, 25_000, 3_000), (2000, 2400, 60_000, 2_000)],
+            [(3000, 3040, 9_000, 500)]]
+    for it, batches in enumerate(plan):
+        for b in batches:
+            series, vals = batch(*b)
+            eng.ingest(series, vals)
+            o.ingest(series, vals)
+        reset = it % 2 == 1
+        got, counts = eng.snapshot(reset=reset, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"snapshot {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=reset), f"split {it}")
+
+
 def test_range_snapshot_peek_export(oracle):
     rng = np.random.default_rng(21)
     S = 500
