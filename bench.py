@@ -34,7 +34,8 @@ KERNEL_ALG_BYTES = {
     # algorithmic bytes per launch, per unit
     "count": lambda n, s: 4 * n,                  # reads series ids
     "bin1": lambda n, s: 8 * n + 4 * n,           # reads (series, value), writes 4-B level-1 record
-    "bin2": lambda n, s: 4 * n + 4 * n,           # reads level-1 record, writes final record
+    # bin2 moves only the records of non-direct tiles (a data-dependent share of n):
+    # it is timed but not priced
     "accum": lambda n, s: 4 * n + 7280 * s,       # reads final record, writes counts + summary
 }
 
