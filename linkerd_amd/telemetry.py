@@ -24,6 +24,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from .javamap import reference_child_order
+
 
 @dataclass(frozen=True)
 class HistogramSummary:
@@ -231,15 +233,20 @@ class MetricsTree:
 
     def __init__(self, engine: Optional[StatEngine] = None):
         self._engine = engine
-        self._trees: Dict[str, "MetricsTree"] = {}
+        self._trees: Dict[str, "MetricsTree"] = {}  # insertion order
+        self._order: Optional[List[str]] = None
         self._tlock = threading.Lock()
         self._mlock = threading.Lock()
         self._metric = Metric.NONE
 
     @property
     def children(self) -> Dict[str, "MetricsTree"]:
+        """Children in the reference's iteration order (ConcurrentHashMap ->
+        immutable Map, MetricsTree.scala:44-45; linkerd_amd.javamap)."""
         with self._tlock:
-            return dict(self._trees)
+            if self._order is None or len(self._order) != len(self._trees):
+                self._order = reference_child_order(list(self._trees))
+            return {k: self._trees[k] for k in self._order}
 
     def _get_or_mk(self, k: str) -> "MetricsTree":
         with self._tlock:
@@ -308,6 +315,7 @@ class MetricsTree:
         with self._tlock:
             kids = list(self._trees.values())
             self._trees.clear()
+            self._order = None
         for k in kids:
             k.prune()
         with self._mlock:

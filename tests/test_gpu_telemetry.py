@@ -99,3 +99,47 @@ def test_c5_prometheus_export_matches_oracle(oracle):
     got, want = prom.render(), PrometheusTelemeter(otree).render()
     assert line_multiset(got) == line_multiset(want)
     assert len(got.splitlines()) == S * 11 + 2000 + 200
+
+
+def test_p4_admin_metrics_json_through_gpu():
+    """AdminMetricsExportTelemeterTest.scala:47-85 end to end: Stat.add -> GPU ->
+    one fused snapshot+reset per interval (tick) -> /admin/metrics.json."""
+    from linkerd_amd.admin_metrics import AdminMetricsExportTelemeter
+    from tests.test_exporters_host import mk_histo_json
+    eng, tree, stats, _ = _setup()
+    tel = AdminMetricsExportTelemeter(tree, 60.0, eng)
+    stat = stats.scope("foo", "bar").stat("bas")
+    stat.add(1.0)
+    assert tel.handle("/admin/metrics.json")[2] == "{}"
+    assert tel.tick() == 1
+    assert tel.handle("/admin/metrics.json")[2] == mk_histo_json("foo/bar/bas", 1)
+    stat.add(2.0)
+    assert tel.handle("/admin/metrics.json")[2] == mk_histo_json("foo/bar/bas", 1)
+    tel.tick()
+    assert tel.handle("/admin/metrics.json")[2] == mk_histo_json("foo/bar/bas", 2)
+
+
+def test_p3_influx_line_through_gpu():
+    """InfluxDbTelemeterTest.scala:141-172 end to end (cumulative Stat.snapshot())."""
+    from linkerd_amd.influxdb import InfluxDbTelemeter
+    eng, tree, stats, _ = _setup()
+    tel = InfluxDbTelemeter(tree)
+    a, d = stats.stat("abc"), stats.stat("def")
+    ma, md = tree.resolve(["abc"]).metric, tree.resolve(["def"]).metric
+    a.add(1.0)
+    d.add(2.0)
+    assert tel.render() == ""
+    ma.snapshot()
+    md.snapshot()
+    assert tel.render() == (
+        "root,host=none abc_avg=1.0,abc_count=1,abc_max=1,abc_min=1,abc_p50=1,abc_p90=1,abc_p95=1,abc_p99=1,"
+        "abc_p999=1,abc_p9999=1,abc_sum=1,def_avg=2.0,def_count=1,def_max=2,def_min=2,def_p50=2,def_p90=2,"
+        "def_p95=2,def_p99=2,def_p999=2,def_p9999=2,def_sum=2\n")
+    a.add(2.0)
+    d.add(4.0)
+    ma.snapshot()
+    md.snapshot()
+    assert tel.render() == (
+        "root,host=none abc_avg=1.5,abc_count=2,abc_max=2,abc_min=1,abc_p50=1,abc_p90=2,abc_p95=2,abc_p99=2,"
+        "abc_p999=2,abc_p9999=2,abc_sum=3,def_avg=3.0,def_count=2,def_max=4,def_min=2,def_p50=2,def_p90=4,"
+        "def_p95=4,def_p99=4,def_p999=4,def_p9999=4,def_sum=6\n")
