@@ -1,7 +1,8 @@
 """Aggregate rocprofv3 --pmc CSVs (tools/profile_pmc.sh) per kernel: average value
 of each counter per dispatch, HBM bytes per launch with the gfx950 corrections of
 MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of wide streaming reads:
-doubled; WRITE_SIZE taken as is; both in KB)."""
+doubled; WRITE_SIZE taken as is; both in KB).  The first dispatch of each kernel
+(no split set yet) is excluded when a kernel has >= 3 dispatches."""
 import csv
 import glob
 import json
@@ -24,7 +25,10 @@ def main(d, out_json=None, meta=None):
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
     for k, cs in sorted(acc.items()):
-        row = {c: sum(v) / len(v) for c, v in cs.items()}
+        # steady state: the first dispatch of a kernel runs before the engine has
+        # a split set (the previous batch's big tiles), so it is dropped when
+        # there are >= 3 dispatches
+        row = {c: (sum(v[1:]) / (len(v) - 1) if len(v) >= 3 else sum(v) / len(v)) for c, v in cs.items()}
         if "FETCH_SIZE" in row or "WRITE_SIZE" in row:
             rd = 2 * 1024 * row.get("FETCH_SIZE", 0.0)
             wr = 1024 * row.get("WRITE_SIZE", 0.0)
