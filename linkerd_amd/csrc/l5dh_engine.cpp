@@ -350,7 +350,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   Plan pl = plan(c);
   {
     KTimer kt(c, L5DH_K_SCAN);
-    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, pl, c->stream));
+    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, c->d_dirty, pl, c->stream));
   }
   HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 16, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

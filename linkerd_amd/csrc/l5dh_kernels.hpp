@@ -31,6 +31,8 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 // LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows
 // (hot), lane-private offset sums, the bucket LUT
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8 + TILE * 8 + 16;
+// cold item of nser series (a tile, or half of one): u16-packed rows, lane-private sums, the LUT, sumfix
+constexpr size_t acc_cold_lds(int nser) { return (size_t)nser * CROW * 4 + nser * 64 * 4 + 1024 * 8 + nser * 8 + 16; }
 // hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
 constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;
@@ -83,6 +85,7 @@ struct State {
 
 constexpr uint8_t TF_SINGLE = 1;   // big tile finished in place by k_accum_hot (one chunk)
 constexpr uint8_t TF_SPLIT = 2;    // big tile accumulated per half (split in every pending segment)
+constexpr uint8_t TF_DIRTY = 4;    // the tile held live counts when k_plan ran
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
@@ -147,8 +150,8 @@ hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, si
 hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
                        const uint32_t* tile_base, const uint32_t* coltot, const uint32_t* split, Tables tb,
                        const uint32_t* stplan, uint32_t* records, int dbg, hipStream_t st);
-hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
-                       hipStream_t st);
+hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
+                       const uint8_t* dirty, Plan plan, hipStream_t st);
 hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,

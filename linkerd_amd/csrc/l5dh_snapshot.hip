@@ -14,12 +14,13 @@ namespace l5dh {
 namespace {
 
 __constant__ int g_dbg;  // L5DH_DBG timing-only variants (results invalid): 0x100 no records, 0x200 no dense stores
+int g_dbg_host = 0;      // host copy of L5DH_DBG (launch-time variants)
 
 // k_plan: one workgroup.  Per tile: records across segments, hot/cold, work
 // items; exclusive scans -> cold_tile[] (item -> tile), hot_item[] (item -> tile
 // and chunk), hot_list, header {cold items, multi-chunk tiles, hot items}.
 __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
-                                               uint32_t hot_chunk, Plan plan) {
+                                               uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
   __shared__ uint32_t lds_a[17];
   __shared__ uint32_t lds_b[17];
   __shared__ uint32_t lds_c[17];
@@ -66,11 +67,11 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     const uint32_t t = t0 + k;
     if (t >= F) break;
     const uint32_t tot = plan.tile_tot[t];
-    uint8_t flags = 0;
+    uint8_t flags = dirty[t] ? TF_DIRTY : 0;
     if (tot > cold_limit) {
       const uint32_t h0 = split_h0(t);
       if (h0 != 0xFFFFFFFFu) {
-        flags = TF_SPLIT;
+        flags |= TF_SPLIT;
         for (uint32_t h = 0; h < 2; ++h) {
           const uint32_t nh = ((h ? tot - h0 : h0) + hot_chunk - 1) / hot_chunk;
           for (uint32_t c = 0; c < nh; ++c) plan.split_item[sa++] = make_uint2(t | (h << 15), c);
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
         const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
         for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
         ha += nc;
-        if (tot <= hot_chunk) flags = TF_SINGLE;
+        if (tot <= hot_chunk) flags |= TF_SINGLE;
       }
       plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
@@ -169,7 +170,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   int64_t total = (int64_t)vsum + fix;  // fix = sumfix[s], read (and cleared) by the caller
   if (dirty) total += st.total[s];
   if (lane == 0 && keep) st.total[s] = total;
-  if (emit) {
+  if (emit && !(g_dbg & 0x40000)) {  // 0x40000 (timing): no summaries
     Summary88* so = out.summ ? out.summ + oi : nullptr;
     if (dirty)
       wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
@@ -200,7 +201,7 @@ __device__ __forceinline__ void count_batch(const uint32_t (&rec)[K], const uint
 }
 
 // Records of tile t in the virtual range [vlo, vhi) of its concatenated segments.
-template <class Fn>
+template <int NT = WG, class Fn>
 __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi, Fn&& fn) {
   uint64_t vbase = 0;
   for (int j = 0; j < segs.n; ++j) {
@@ -211,7 +212,7 @@ __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, u
     const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
     if (lo < hi) {
       const uint32_t ra = a + (uint32_t)(lo - vbase);
-      for_records<WG>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), fn);
+      for_records<NT>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), fn);
     }
     vbase += len;
   }
@@ -274,95 +275,98 @@ __device__ __forceinline__ void for_half_records(const Segs& segs, uint32_t t, u
   }
 }
 
-// k_accum: one work item =
-//   cold tile (<= cold_limit records): 32 series in u16-packed LDS bins, one pass;
-//   warm tile (<= hot_chunk records): two rounds (series 0-15, 16-31) in u32 LDS
-//     bins over the same records (the second read hits L2), outputs in place;
-//   hot chunk (hot_chunk records of a bigger tile): the same two rounds, each
-//     flushed with global atomics into the state rows (k_hot_finish completes).
-__global__ __launch_bounds__(WG) void k_accum_cold(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                              uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset) {
+// k_accum_cold: one work item = the series of a cold tile (<= cold_limit records)
+// in u16-packed LDS bins, one pass over the tile's records, then one wave per
+// series emits the dense row and the summary.  NSER = 16: the item is one half of
+// the tile, so two 512-thread workgroups of 70 KB share a CU and one's emission
+// overlaps the other's counting; the two halves of a tile are blocks b and b+8,
+// which the round-robin dispatch puts on the same XCD, so the second read of the
+// tile's records mostly hits that XCD's L2 (speed only).  NSER = 32: the whole
+// tile in one 1024-thread workgroup.
+template <int NSER, int NT>
+__global__ __launch_bounds__(NT, 4) void k_accum_cold(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                                   uint32_t cold_items, int final_mode, int reset) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t item = blockIdx.x;
+  uint32_t item = blockIdx.x, half = 0;
+  if (NSER == 16) {
+    item = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);
+    half = (blockIdx.x / 8) & 1u;
+  }
+  if (item >= cold_items) return;
   const uint32_t t = plan.cold_tile[item];
-  const uint32_t tot = plan.tile_tot[t];
   const int w = threadIdx.x >> 6;
   const bool keep = !(final_mode && reset);
-
-  {
-    uint32_t* hist = smem;                    // [32][900] u16 pairs
-    uint32_t* vsl = smem + TILE * CROW;       // [32][64] lane-private value sums (< 1152 x 2^21 per slot)
-    uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);  // [LUT2_N]
-    int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the tile's series
-    uint32_t* dirtyl = reinterpret_cast<uint32_t*>(fixl + TILE);
-    const int lane = lane_id();
-    auto count = [&](uint32_t rec) {
-      const uint32_t loc = (rec >> 21) & 31u;
-      uint32_t v;
-      const uint32_t b = record_bucket(rec, lut2, v);
-      atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-      atomicAdd(&vsl[loc * 64 + lane], v);  // no same-address lanes
-    };
-    // one pending segment (the common case): the tile's first 8 records per lane
-    // are loaded before the LDS is cleared, so their latency overlaps the clearing
-    const bool one = segs.n == 1 && !(g_dbg & 0x100);
-    const uint32_t a = one ? segs.tbase[0][t] : 0u, e = one ? segs.tbase[0][t + 1] : 0u;  // no segment: no read
-    const uint32_t a4 = a & ~3u;
-    auto ld = [&](uint32_t g) {
-      return g < e ? *reinterpret_cast<const uint4*>(segs.recs[0] + g) : make_uint4(0u, 0u, 0u, 0u);
-    };
-    uint32_t g = a4 + 4u * threadIdx.x;
-    uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
-    if (one) {
-      n0 = ld(g);
-      n1 = ld(g + 4u * WG);
-    }
-    if (threadIdx.x < TILE) {  // the tile's sumfix entries (read and cleared here) and dirty flag
-      const uint32_t s = t * TILE + threadIdx.x;
-      int64_t f = 0;
-      if (s < st.S) {
-        f = st.sumfix[s];
-        if (f) st.sumfix[s] = 0;
-      }
-      fixl[threadIdx.x] = f;
-      if (threadIdx.x == 0) dirtyl[0] = st.dirty[t];
-    }
-    {
-      uint4* p = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64) / 4; i += WG) p[i] = make_uint4(0, 0, 0, 0);
-      for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
-    }
-    __syncthreads();
-    if (one) {
-      for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
-        const uint4 x0 = n0, x1 = n1;
-        n0 = ld(g + 8u * WG);
-        n1 = ld(g + 12u * WG);
-        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
-          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
-        }
-        count_batch<8>(
-            x, lut2, [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u); },
-            [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[loc * 64 + lane], v); });
-      }
-    } else if (!(g_dbg & 0x100)) {
-      for_tile_records(segs, t, 0, tot, count);
-    }
-    __syncthreads();
-    const bool dirty = dirtyl[0] != 0;
-    for (int rep = 0; rep < 2; ++rep) {
-      const uint32_t loc = w + 16 * rep;
-      const uint32_t s = t * TILE + loc;
-      if (s >= st.S) continue;
-      const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
-      emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dirty, keep, final_mode, st, tb, out);
-    }
-    if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
+  const uint32_t s0 = t * TILE + half * 16;  // first series of the item
+  uint32_t* hist = smem;                     // [NSER][900] u16 pairs
+  uint32_t* vsl = smem + NSER * CROW;        // [NSER][64] lane-private value sums (< 1152 x 2^21 per slot)
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
+  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [NSER] sumfix of the item's series
+  const int lane = lane_id();
+  // a record of the tile's other half (NSER = 16) counts as no record
+  auto own = [&](uint32_t rec) {
+    return (NSER == 32 || ((rec >> 25) & 1u) == half) ? rec : 0xFFFFFFFFu;
+  };
+  auto hist_add = [&](uint32_t loc, uint32_t b) {
+    atomicAdd(&hist[(loc & (NSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+  };
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & (NSER - 1)) * 64 + lane], v); };
+  // one pending segment (the common case): the tile's first 8 records per lane
+  // are loaded before the LDS is cleared, so their latency overlaps the clearing
+  const bool one = segs.n == 1 && !(g_dbg & 0x100);
+  const uint32_t a = one ? segs.tbase[0][t] : 0u, e = one ? segs.tbase[0][t + 1] : 0u;  // no segment: no read
+  const uint32_t a4 = a & ~3u;
+  auto ld = [&](uint32_t g) {
+    return g < e ? *reinterpret_cast<const uint4*>(segs.recs[0] + g) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  uint32_t g = a4 + 4u * threadIdx.x;
+  uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+  if (one) {
+    n0 = ld(g);
+    n1 = ld(g + 4u * NT);
   }
-
+  if (threadIdx.x < NSER) {  // the item's sumfix entries (read and cleared here)
+    const uint32_t s = s0 + threadIdx.x;
+    int64_t f = 0;
+    if (s < st.S) {
+      f = st.sumfix[s];
+      if (f) st.sumfix[s] = 0;
+    }
+    fixl[threadIdx.x] = f;
+  }
+  {
+    uint4* p = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < (NSER * CROW + NSER * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+  }
+  __syncthreads();
+  if (one) {
+    for (uint32_t c = a4; c < e; c += 8u * NT, g += 8u * NT) {
+      const uint4 x0 = n0, x1 = n1;
+      n0 = ld(g + 8u * NT);
+      n1 = ld(g + 12u * NT);
+      uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t gk = g + (k >> 2) * 4u * NT + (k & 3);
+        x[k] = (gk < a || gk >= e) ? 0xFFFFFFFFu : own(x[k]);
+      }
+      count_batch<8>(x, lut2, hist_add, sum_add);
+    }
+  } else if (!(g_dbg & 0x100)) {
+    for_tile_records<NT>(segs, t, 0, plan.tile_tot[t], [&](uint32_t rec) {
+      const uint32_t x[1] = {own(rec)};
+      count_batch<1>(x, lut2, hist_add, sum_add);
+    });
+  }
+  __syncthreads();
+  const bool dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;  // as of k_plan: both halves see the same
+  for (int loc = w; loc < NSER; loc += NT / 64) {
+    const uint32_t s = s0 + loc;
+    if (s >= st.S) continue;
+    const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
+    emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dirty, keep, final_mode, st, tb, out);
+  }
+  if (threadIdx.x == 0 && half == 0) st.dirty[t] = keep ? 1 : 0;
 }
 
 // Big tiles (> cold_limit records): item = (chunk of <= hot_chunk records, half of
@@ -589,19 +593,26 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
 
 }  // namespace
 
-hipError_t set_snapshot_debug(int dbg) { return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dbg, sizeof(int)); }
+hipError_t set_snapshot_debug(int dbg) {
+  g_dbg_host = dbg;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dbg, sizeof(int));
+}
 
 hipError_t set_snapshot_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)acc_cold_lds(32));
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_cold<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)acc_cold_lds(16));
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
 }
 
-hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk, Plan plan,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
+hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
+                       const uint8_t* dirty, Plan plan, hipStream_t st) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
   return hipGetLastError();
 }
 
@@ -615,8 +626,15 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st) {
   if (cold_items) {
-    hipLaunchKernelGGL(k_accum_cold, dim3(cold_items), dim3(WG), ACC_LDS, st, segs, plan, state, tb, out, cold_limit,
-                       hot_chunk, final_mode, reset);
+    // whole tiles, one 1024-thread workgroup per CU; L5DH_DBG bit 0x20000: half-tile
+    // items, two 512-thread workgroups per CU (measured slower, alone and next to the
+    // split items; so was a persistent form that prefetches the next tile's records)
+    if (!(g_dbg_host & 0x20000))
+      hipLaunchKernelGGL((k_accum_cold<32, 1024>), dim3(cold_items), dim3(1024), acc_cold_lds(32), st, segs, plan,
+                         state, tb, out, cold_items, final_mode, reset);
+    else
+      hipLaunchKernelGGL((k_accum_cold<16, 512>), dim3(((cold_items + 7) / 8) * 16), dim3(512), acc_cold_lds(16), st,
+                         segs, plan, state, tb, out, cold_items, final_mode, reset);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
