@@ -63,7 +63,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
         const uint32_t sv[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
         uint2 wv[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) wv[k] = sw[min(sv[k], S - 1) >> (TILE_SHIFT + 5)];
+        for (int k = 0; k < 16; ++k) wv[k] = sw[(sv[k] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
         uint32_t key[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 // written in order.  Batches are < 2^30 samples.
 // LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, direct
 // words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
-template <int CH1, int NT, int WPS>
+template <int CH1, int NT, int WPS, bool HS>
 __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                 size_t n, size_t per, uint32_t S, uint32_t F,
                                                 const uint32_t* __restrict__ pre,
@@ -354,8 +354,10 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       uint32_t escm = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        // fast: +0 <= f < V_ESC, one integer compare of the bit pattern (-0, NaN and
+        // (-1, 0) take the exact slow path, which also truncates them to 0)
         const float f = fv[g + q];
-        const bool fast = f >= 0.0f && f < (float)V_ESC;
+        const bool fast = __float_as_uint(f) < 0x49FFC000u;  // bits of (float)V_ESC
         pl[q] = fast ? (uint32_t)f : 0u;
         escm |= (!fast && sv[g + q] < S) ? (1u << q) : 0u;
       }
@@ -375,39 +377,46 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       }
       uint2 dv[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dv[q] = dw[min(sv[g + q], S - 1) >> (TILE_SHIFT + 5)];
+      for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
       uint32_t bn[4], sl[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t s = sv[g + q];
-        const uint32_t t = s >> TILE_SHIFT;
-        const uint32_t bit = 1u << (t & 31u);
-        const bool direct = (dv[q].x & bit) != 0u;
-        rec[g + q] = ((t & (ST_TILES - 1)) << 26) | ((s & (TILE - 1)) << 21) | pl[q];
-        const uint32_t dbin = FS + 2u * (dv[q].y + (uint32_t)__popc(dv[q].x & (bit - 1u))) + ((s >> 4) & 1u);
+        const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);  // tile within its direct word
+        const bool direct = __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
+        rec[g + q] = ((s & (ST_TILES * TILE - 1)) << 21) | pl[q];  // tile in ST | series in tile | payload
+        const uint32_t dbin =
+            FS + 2u * (dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw))) + ((s >> 4) & 1u);
         bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
       }
+      if (HS) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sl[q] = hslot[bn[q]];
+        for (int q = 0; q < 4; ++q) sl[q] = hslot[bn[q]];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool hot = sl[q] < (uint32_t)NHOT;
-        uint32_t* ctr = hot ? hcnt + sl[q] * 64u + (uint32_t)lane : cnt + bn[q];
-        pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
+        for (int q = 0; q < 4; ++q) {
+          const bool hot = sl[q] < (uint32_t)NHOT;
+          uint32_t* ctr = hot ? hcnt + sl[q] * 64u + (uint32_t)lane : cnt + bn[q];
+          pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
     __syncthreads();
     if (wv == 0) {  // one wave: hot-slot lane prefixes and totals, then the bin scan (DPP, no barriers)
-      uint32_t hv[NHOT];
+      if (HS) {
+        uint32_t hv[NHOT];
 #pragma unroll
-      for (int h = 0; h < NHOT; ++h) hv[h] = hcnt[h * 64 + lane];  // rows of unused slots are zero
+        for (int h = 0; h < NHOT; ++h) hv[h] = hcnt[h * 64 + lane];  // rows of unused slots are zero
 #pragma unroll
-      for (int h = 0; h < NHOT; ++h) {
-        const uint32_t x = wave_incl_scan32(hv[h]);
-        hcnt[h * 64 + lane] = x - hv[h];
-        const uint32_t hk = plan[3 * FS + 1 + h];
-        if (lane == 63 && hk != NOKEY) cnt[hk] = x;
+        for (int h = 0; h < NHOT; ++h) {
+          const uint32_t x = wave_incl_scan32(hv[h]);
+          hcnt[h * 64 + lane] = x - hv[h];
+          const uint32_t hk = plan[3 * FS + 1 + h];
+          if (lane == 63 && hk != NOKEY) cnt[hk] = x;
+        }
       }
       uint32_t c[16];  // lane l scans bins [16 l, 16 l + 16)
 #pragma unroll
@@ -429,7 +438,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = (pk[k] >> 14) & 2047u;
-      const uint32_t r = (pk[k] & 16383u) + hcnt[(pk[k] >> 25) * 64 + lane];  // row NHOT is zero
+      const uint32_t r = (pk[k] & 16383u) + (HS ? hcnt[(pk[k] >> 25) * 64 + lane] : 0u);  // row NHOT is zero
       const uint2 x = oc[bin];
       stage[x.x + r] = make_uint2(rec[k], x.y + r);
     }
@@ -439,7 +448,8 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       cnt[j] = 0;
     }
     if (threadIdx.x == 0) cnt[TB] = 0;
-    for (uint32_t i = threadIdx.x; i < NHOT * 64; i += NT) hcnt[i] = 0;
+    if (HS)
+      for (uint32_t i = threadIdx.x; i < NHOT * 64; i += NT) hcnt[i] = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
       const uint2 e = stage[threadIdx.x + k * NT];
@@ -835,10 +845,13 @@ hipError_t set_ingest_attributes() {
   const int big = 160 * 1024;
   if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bin1_lds(16384))))
+    return e;
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 512, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bin1_lds(6144))))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bin1_lds(16384))))
     return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin2<8192, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -901,10 +914,13 @@ hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, si
   // default -- longer runs per bin beat the second workgroup's overlap (measured);
   // L5DH_DBG bit 20 selects (6144, 512, 2 workgroups/CU)
   if ((dbg >> 20) & 1)
-    hipLaunchKernelGGL((k_bin1<6144, 512, 4>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
+    hipLaunchKernelGGL((k_bin1<6144, 512, 4, true>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
                        pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
+  else if ((dbg >> 22) & 1)  // bit 22: no lane-private hot-bin slots
+    hipLaunchKernelGGL((k_bin1<16384, 1024, 4, false>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
+                       F, pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   else
-    hipLaunchKernelGGL((k_bin1<16384, 1024, 4>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
+    hipLaunchKernelGGL((k_bin1<16384, 1024, 4, true>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
                        F, pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
   return hipGetLastError();
 }
