@@ -592,7 +592,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * (F + COLS) * 4) &&
             mal((void**)&c->d_tile_tot, (F + COLS) * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
-            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, 16) &&
+            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) &&
             mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
             mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT);
   for (int j = 0; ok && j < MAX_SEG; ++j)

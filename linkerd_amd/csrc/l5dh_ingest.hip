@@ -110,64 +110,82 @@ __global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, 
   const int gper = (G + 15) / 16;
   const int g0 = w * gper;
   const int g1 = min(G, g0 + gper);
+  // G <= 512: a wave's <= 32 slabs are loaded at once (one memory latency, not one
+  // per slab: the in-place prefix stores would otherwise order every load)
+  constexpr int GW = 32;
+  uint32_t v[GW];
   uint32_t s = 0;
-  if (t < C)
-    for (int g = g0; g < g1; ++g) s += table[(size_t)g * C + t];
+#pragma unroll
+  for (int k = 0; k < GW; ++k) {
+    v[k] = (t < C && g0 + k < g1) ? table[(size_t)(g0 + k) * C + t] : 0u;
+    s += v[k];
+  }
   part[w][lane] = s;
   __syncthreads();
   if (w == 0) {
     uint32_t acc = 0;
     for (int k = 0; k < 16; ++k) {
-      const uint32_t v = part[k][lane];
+      const uint32_t x = part[k][lane];
       part[k][lane] = acc;
-      acc += v;
+      acc += x;
     }
     if (t < C) tile_tot[t] = acc;
   }
   __syncthreads();
   if (t < C) {
     uint32_t acc = part[w][lane];
-    for (int g = g0; g < g1; ++g) {
-      const size_t i = (size_t)g * C + t;
-      const uint32_t v = table[i];
-      table[i] = acc;
-      acc += v;
-    }
+#pragma unroll
+    for (int k = 0; k < GW; ++k)
+      if (g0 + k < g1) {
+        table[(size_t)(g0 + k) * C + t] = acc;
+        acc += v[k];
+      }
   }
 }
-
-// Tile totals (a split tile's own column is empty: its total is its two half
-// columns, written back to coltot[t]) and their exclusive scan tile_base[F+1].
 __global__ __launch_bounds__(1024) void k_tilescan(uint32_t* __restrict__ coltot, uint32_t F,
                                                    const uint32_t* __restrict__ split, uint32_t* __restrict__ tile_base) {
   __shared__ uint32_t lds[17];
   const uint32_t per = (F + 1023) / 1024;
   const uint32_t t0 = threadIdx.x * per;
-  uint32_t s = 0;
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t t = t0 + k;
-    if (t >= F) break;
+  // a thread's tiles: totals of split tiles are the sums of their halves
+  auto tile_total = [&](uint32_t t, uint32_t v) {
     const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
     const uint32_t bit = 1u << (t & 31u);
-    uint32_t v = coltot[t];
     if (wd & bit) {
       const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
       v += coltot[F + 2 * si] + coltot[F + 2 * si + 1];
       coltot[t] = v;
     }
-    s += v;
-  }
-  uint32_t tot;
-  uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
-  for (uint32_t k = 0; k < per; ++k)
-    if (t0 + k < F) {
+    return v;
+  };
+  constexpr int PT = 32;  // F <= 32 K tiles: all of a thread's loads issued at once
+  uint32_t v[PT];
+  uint32_t s = 0, tot;
+  if (per <= PT) {
+#pragma unroll
+    for (int k = 0; k < PT; ++k) v[k] = ((uint32_t)k < per && t0 + k < F) ? coltot[t0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      if ((uint32_t)k < per && t0 + k < F) v[k] = tile_total(t0 + k, v[k]);
+      s += v[k];
+    }
+    uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
+#pragma unroll
+    for (int k = 0; k < PT; ++k)
+      if ((uint32_t)k < per && t0 + k < F) {
+        tile_base[t0 + k] = acc;
+        acc += v[k];
+      }
+  } else {
+    for (uint32_t k = 0; k < per && t0 + k < F; ++k) s += tile_total(t0 + k, coltot[t0 + k]);
+    uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
+    for (uint32_t k = 0; k < per && t0 + k < F; ++k) {
       tile_base[t0 + k] = acc;
       acc += coltot[t0 + k];
     }
+  }
   if (threadIdx.x == 0) tile_base[F] = tot;
 }
-
-// Segment split info (l5dh_kernels.hpp) from the batch's split set.
 __global__ __launch_bounds__(1024) void k_seginfo(const uint32_t* __restrict__ split, const uint32_t* __restrict__ coltot,
                                                   uint32_t F, uint32_t* __restrict__ sinfo) {
   const uint32_t NS = split[0];
@@ -526,23 +544,37 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     const uint32_t t1 = min(F, (j + 1) * ST_TILES);
     uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest level-1 tiles of this super-tile
     uint32_t a0 = 0, a1 = 0, k0 = 0xFF, k1 = 0xFF;  // two biggest tiles
-    for (uint32_t t = j * ST_TILES; t < t1; ++t) {
-      const uint32_t v = coltot[t];
-      const uint32_t tl = t - j * ST_TILES;
-      tot += v;
-      if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
-      else if (v > a1) { a1 = v; k1 = tl; }
-      if (v >= thr_s) {
-        if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
+    // the super-tile's 64 totals in 16 loads issued at once (coltot holds F + COLS
+    // words, so the reads past F stay in bounds; those tiles are skipped)
+    uint32_t cv[ST_TILES];
+    const uint4* c4 = reinterpret_cast<const uint4*>(coltot + j * ST_TILES);
+#pragma unroll
+    for (int q = 0; q < ST_TILES / 4; ++q) {
+      const uint4 x = c4[q];
+      cv[4 * q] = x.x;
+      cv[4 * q + 1] = x.y;
+      cv[4 * q + 2] = x.z;
+      cv[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (uint32_t tl = 0; tl < (uint32_t)ST_TILES; ++tl) {
+      if (j * ST_TILES + tl < t1) {
+        const uint32_t v = cv[tl];
+        tot += v;
+        if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
+        else if (v > a1) { a1 = v; k1 = tl; }
+        if (v >= thr_s) {
+          if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
+        }
+        const bool split = ((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u;
+        if (split && v >= thr_d) {  // direct: no level-1 records
+          if (tl < 32) d0 |= 1u << tl; else d1 |= 1u << (tl - 32);
+        } else {
+          ctot += v;
+          if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
+          else if (v > b1) { b1 = v; i1 = tl; }
+        }
       }
-      const bool split = ((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u;
-      if (split && v >= thr_d) {  // direct: no level-1 records
-        if (tl < 32) d0 |= 1u << tl; else d1 |= 1u << (tl - 32);
-        continue;
-      }
-      ctot += v;
-      if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
-      else if (v > b1) { b1 = v; i1 = tl; }
     }
     nn = (uint32_t)(__popc(n0) + __popc(n1));
     ndt = (uint32_t)(__popc(d0) + __popc(d1));

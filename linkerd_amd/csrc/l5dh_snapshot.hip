@@ -96,6 +96,114 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
   }
 }
 
+// The same plan from ceil(F / 1024) workgroups (k_plan's single workgroup walks
+// ~31 strided tiles per thread and is latency-bound): k_plan_a classifies tile
+// t = 1024 b + thread with coalesced reads and stores its workgroup's four item
+// counts in header[4 + k B + b]; k_plan_b scans those, rebuilds each tile's class
+// from tile_tot and writes the lists in tile order (the same order as k_plan).
+struct PlanCls {
+  uint32_t ci, hi, hot, si, h0;
+};
+__device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t t, uint32_t tot, int final_mode,
+                                                 uint32_t cold_limit, uint32_t hot_chunk) {
+  PlanCls r{0u, 0u, 0u, 0u, 0xFFFFFFFFu};
+  if (tot > cold_limit) {
+    r.hot = 1;
+    uint32_t h0 = segs.n == 0 ? 0xFFFFFFFFu : 0u;
+    for (int j = 0; j < segs.n; ++j) {
+      const uint16_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
+      if (m == NO_SPLIT) {
+        h0 = 0xFFFFFFFFu;
+        break;
+      }
+      h0 += segs.sinfo[j][SINFO_H0 + m];
+    }
+    r.h0 = h0;
+    if (h0 != 0xFFFFFFFFu)
+      r.si = (h0 + hot_chunk - 1) / hot_chunk + (tot - h0 + hot_chunk - 1) / hot_chunk;
+    else
+      r.hi = (tot + hot_chunk - 1) / hot_chunk;
+  } else if (final_mode || tot > 0) {
+    r.ci = 1;
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
+                                                 uint32_t hot_chunk, Plan plan) {
+  __shared__ uint32_t red[4][17];
+  const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
+  PlanCls c{0u, 0u, 0u, 0u, 0u};
+  if (t < F) {
+    uint32_t tot = 0;
+    for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
+    plan.tile_tot[t] = tot;
+    c = plan_classify(segs, t, tot, final_mode, cold_limit, hot_chunk);
+  }
+  const uint32_t v[4] = {c.ci, c.hot, c.hi, c.si};  // header order
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = wave_sum((uint64_t)v[k]);
+    if (lane == 0) red[k][w] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint32_t x = 0;
+    for (int q = 0; q < 16; ++q) x += red[threadIdx.x][q];
+    plan.header[4 + threadIdx.x * gridDim.x + blockIdx.x] = x;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
+                                                 uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
+  __shared__ uint32_t lds[4][17];
+  __shared__ uint32_t base[4];
+  const uint32_t B = gridDim.x;
+  // workgroup bases: exclusive sums of the earlier workgroups' counts (B <= 1024 x 1024 tiles)
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
+    const uint32_t y = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
+    uint32_t tx = 0, ty = 0;
+    block_excl_scan<1024>(x, lds[k], &tx);
+    if (blockIdx.x == 0) block_excl_scan<1024>(y, lds[k], &ty);
+    if (threadIdx.x == 0) {
+      base[k] = tx;
+      if (blockIdx.x == 0) plan.header[k] = ty;  // header: cold items, big tiles, mixed-half items, split items
+    }
+  }
+  __syncthreads();
+  const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
+  PlanCls c{0u, 0u, 0u, 0u, 0xFFFFFFFFu};
+  uint32_t tot = 0;
+  if (t < F) {
+    tot = plan.tile_tot[t];
+    c = plan_classify(segs, t, tot, final_mode, cold_limit, hot_chunk);
+  }
+  uint32_t ca = base[0] + block_excl_scan<1024>(c.ci, lds[0], nullptr);
+  const uint32_t xa = base[1] + block_excl_scan<1024>(c.hot, lds[1], nullptr);
+  uint32_t ha = base[2] + block_excl_scan<1024>(c.hi, lds[2], nullptr);
+  uint32_t sa = base[3] + block_excl_scan<1024>(c.si, lds[3], nullptr);
+  if (t >= F) return;
+  uint8_t flags = dirty[t] ? TF_DIRTY : 0;
+  if (c.hot) {
+    if (c.h0 != 0xFFFFFFFFu) {
+      flags |= TF_SPLIT;
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
+        for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
+      }
+    } else {
+      for (uint32_t q = 0; q < c.hi; ++q) plan.hot_item[ha + q] = t | (q << 15);
+      if (tot <= hot_chunk) flags |= TF_SINGLE;
+    }
+    plan.hot_list[xa] = t;
+  } else if (c.ci) {
+    plan.cold_tile[ca] = t;
+  }
+  plan.tile_flags[t] = flags;
+}
+
 // k_hot_init: split tiles accumulate with global atomics into state rows, so
 // clean ones start from zero.
 __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t hot_chunk) {
@@ -369,6 +477,108 @@ __global__ __launch_bounds__(NT, 4) void k_accum_cold(Segs segs, Plan plan, Stat
   if (threadIdx.x == 0 && half == 0) st.dirty[t] = keep ? 1 : 0;
 }
 
+// k_accum_cold_p: the persistent form of k_accum_cold<32>.  One 1024-thread
+// workgroup per CU walks the cold items blockIdx.x, + gridDim.x, ...: the LUT is
+// staged once, each wave clears its series' LDS rows right after emitting them
+// (no clearing phase), and the next item's record range, first 8 records per
+// lane, sumfix entries and dirty flag are loaded before the current item's
+// emission, so their latency hides behind it (and behind its dense stores).
+template <int NT>
+__global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                                      uint32_t cold_items, int final_mode, int reset) {
+  constexpr int NSER = 32;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* hist = smem;                                      // [32][900] u16 pairs
+  uint32_t* vsl = smem + NSER * CROW;                         // [32][64] lane-private value sums
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
+  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the item's series
+  const int w = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const bool keep = !(final_mode && reset);
+  const bool one = segs.n == 1 && !(g_dbg & 0x100);
+  const uint32_t* __restrict__ r0 = segs.recs[0];
+  auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u); };
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[loc * 64 + lane], v); };
+  auto ld = [&](uint32_t g, uint32_t e) {
+    return g < e ? *reinterpret_cast<const uint4*>(r0 + g) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  {
+    uint4* p = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < (NSER * CROW + NSER * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+  }
+  // the next item: tile, record range, first records, sumfix entry, dirty flag
+  uint32_t item = blockIdx.x;
+  uint32_t t = 0, a = 0, e = 0;
+  uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
+  int64_t f = 0;
+  bool dirty = false;
+  auto fetch = [&](uint32_t it) {
+    if (it >= cold_items) return;
+    t = plan.cold_tile[it];
+    dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;
+    if (one) {
+      a = segs.tbase[0][t];
+      e = segs.tbase[0][t + 1];
+      const uint32_t g = (a & ~3u) + 4u * threadIdx.x;
+      n0 = ld(g, e);
+      n1 = ld(g + 4u * NT, e);
+    }
+    if (threadIdx.x < NSER) {
+      const uint32_t s = t * TILE + threadIdx.x;
+      f = 0;
+      if (s < st.S) {
+        f = st.sumfix[s];
+        if (f) st.sumfix[s] = 0;
+      }
+    }
+  };
+  fetch(item);
+  __syncthreads();
+  for (; item < cold_items; item += gridDim.x) {
+    const uint32_t tc = t;
+    const bool dc = dirty;
+    if (threadIdx.x < NSER) fixl[threadIdx.x] = f;
+    if (one) {
+      const uint32_t a4 = a & ~3u;
+      uint32_t g = a4 + 4u * threadIdx.x;
+      for (uint32_t c = a4; c < e; c += 8u * NT, g += 8u * NT) {
+        const uint4 x0 = n0, x1 = n1;
+        n0 = ld(g + 8u * NT, e);
+        n1 = ld(g + 12u * NT, e);
+        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t gk = g + (k >> 2) * 4u * NT + (k & 3);
+          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+        }
+        count_batch<8>(x, lut2, hist_add, sum_add);
+      }
+    } else if (!(g_dbg & 0x100)) {
+      for_tile_records<NT>(segs, tc, 0, plan.tile_tot[tc], [&](uint32_t rec) {
+        const uint32_t x[1] = {rec};
+        count_batch<1>(x, lut2, hist_add, sum_add);
+      });
+    }
+    __syncthreads();  // counts complete; fixl visible
+    fetch(item + gridDim.x);
+    const uint32_t s0 = tc * TILE;
+    for (int loc = w; loc < NSER; loc += NT / 64) {
+      const uint32_t s = s0 + loc;
+      if (s < st.S) {
+        const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
+        emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dc, keep, final_mode, st, tb, out);
+      }
+      // this wave owns the row: clear it for the next item (LDS ops of a wave stay in order)
+      uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
+      for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      vsl[loc * 64 + lane] = 0u;
+    }
+    if (threadIdx.x == 0) st.dirty[tc] = keep ? 1 : 0;
+    __syncthreads();  // rows cleared, fixl consumed
+  }
+}
+
 // Big tiles (> cold_limit records): item = (chunk of <= hot_chunk records, half of
 // the tile's series).  Both halves of a chunk are blocks b and b+8 -- the same XCD
 // under the round-robin dispatch (MI355X_MICROARCH.md), so they stream the chunk
@@ -602,6 +812,9 @@ hipError_t set_snapshot_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)acc_cold_lds(32));
   if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_cold_p<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)acc_cold_lds(32));
+  if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_cold<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)acc_cold_lds(16));
   if (e != hipSuccess) return e;
@@ -612,7 +825,15 @@ hipError_t set_snapshot_attributes() {
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
                        const uint8_t* dirty, Plan plan, hipStream_t st) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
+  // single-workgroup plan past 2^20 tiles (k_plan_b scans <= 1024 workgroup counts),
+  // or with L5DH_DBG bit 0x1000000
+  if ((g_dbg_host & 0x1000000) || F > (1u << 20)) {
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
+    return hipGetLastError();
+  }
+  const uint32_t B = (F + 1023) / 1024;  // header holds 4 + 4 B words (l5dh_engine.cpp)
+  hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
+  hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
   return hipGetLastError();
 }
 
@@ -626,10 +847,22 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st) {
   if (cold_items) {
-    // whole tiles, one 1024-thread workgroup per CU; L5DH_DBG bit 0x20000: half-tile
-    // items, two 512-thread workgroups per CU (measured slower, alone and next to the
-    // split items; so was a persistent form that prefetches the next tile's records)
-    if (!(g_dbg_host & 0x20000))
+    // default: the persistent form, one 1024-thread workgroup per CU walking the cold
+    // tiles (-3 % against a workgroup per tile, measured).  L5DH_DBG bit 0x800000: a
+    // workgroup per tile; with bit 0x20000 also: half-tile items, two 512-thread
+    // workgroups per CU (measured slower, alone and next to the split items)
+    if (!(g_dbg_host & 0x800000)) {
+      static int ncu = 0;
+      if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+          ncu = 256;
+      }
+      const uint32_t grid = cold_items < (uint32_t)ncu ? cold_items : (uint32_t)ncu;
+      hipLaunchKernelGGL((k_accum_cold_p<1024>), dim3(grid), dim3(1024), acc_cold_lds(32), st, segs, plan, state, tb,
+                         out, cold_items, final_mode, reset);
+    } else if (!(g_dbg_host & 0x20000))
       hipLaunchKernelGGL((k_accum_cold<32, 1024>), dim3(cold_items), dim3(1024), acc_cold_lds(32), st, segs, plan,
                          state, tb, out, cold_items, final_mode, reset);
     else
