@@ -33,6 +33,7 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8 + TILE * 8 + 16;
 // cold item of nser series (a tile, or half of one): u16-packed rows, lane-private sums, the LUT, sumfix
 constexpr size_t acc_cold_lds(int nser) { return (size_t)nser * CROW * 4 + nser * 64 * 4 + 1024 * 8 + nser * 8 + 16; }
+constexpr size_t acc_cold_p_lds(int nser) { return acc_cold_lds(nser) + ROW * 4; }  // + bucket midpoints
 // hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
 constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;

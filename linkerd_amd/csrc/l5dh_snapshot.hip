@@ -477,28 +477,43 @@ __global__ __launch_bounds__(NT, 4) void k_accum_cold(Segs segs, Plan plan, Stat
   if (threadIdx.x == 0 && half == 0) st.dirty[t] = keep ? 1 : 0;
 }
 
-// k_accum_cold_p: the persistent form of k_accum_cold<32>.  One 1024-thread
-// workgroup per CU walks the cold items blockIdx.x, + gridDim.x, ...: the LUT is
+// k_accum_cold_p: the persistent form of k_accum_cold.  NSER = 32: one 1024-thread
+// workgroup per CU walks the cold items blockIdx.x, + gridDim.x, ...; NSER = 16:
+// two 512-thread workgroups per CU, one half-tile each.  The LUT is
 // staged once, each wave clears its series' LDS rows right after emitting them
 // (no clearing phase), and the next item's record range, first 8 records per
 // lane, sumfix entries and dirty flag are loaded before the current item's
 // emission, so their latency hides behind it (and behind its dense stores).
-template <int NT>
+template <int NSER, int NT>
 __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                       uint32_t cold_items, int final_mode, int reset) {
-  constexpr int NSER = 32;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* hist = smem;                                      // [32][900] u16 pairs
-  uint32_t* vsl = smem + NSER * CROW;                         // [32][64] lane-private value sums
+  uint32_t* hist = smem;                                      // [NSER][900] u16 pairs
+  uint32_t* vsl = smem + NSER * CROW;                         // [NSER][64] lane-private value sums
   uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
-  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the item's series
+  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [NSER] sumfix of the item's series
+  int32_t* midl = reinterpret_cast<int32_t*>(fixl + NSER);     // [NB] bucket midpoints (the summary's lookups)
   const int w = threadIdx.x >> 6;
   const int lane = lane_id();
   const bool keep = !(final_mode && reset);
   const bool one = segs.n == 1 && !(g_dbg & 0x100);
   const uint32_t* __restrict__ r0 = segs.recs[0];
-  auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[loc * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u); };
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[loc * 64 + lane], v); };
+  Tables tbl = tb;
+  tbl.mid = midl;
+  // NSER = 16: blocks b and b + 8 (same XCD under the round-robin dispatch) walk the
+  // same tiles, one half each, so a tile's records are read from HBM about once
+  uint32_t first = blockIdx.x, stride = gridDim.x, half = 0;
+  if (NSER == 16) {
+    first = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);
+    half = (blockIdx.x / 8) & 1u;
+    stride = gridDim.x / 2;
+  }
+  // a record of the tile's other half counts as no record
+  auto own = [&](uint32_t rec) { return (NSER == 32 || ((rec >> 25) & 1u) == half) ? rec : 0xFFFFFFFFu; };
+  auto hist_add = [&](uint32_t loc, uint32_t b) {
+    atomicAdd(&hist[(loc & (NSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+  };
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & (NSER - 1)) * 64 + lane], v); };
   auto ld = [&](uint32_t g, uint32_t e) {
     return g < e ? *reinterpret_cast<const uint4*>(r0 + g) : make_uint4(0u, 0u, 0u, 0u);
   };
@@ -506,9 +521,10 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
     uint4* p = reinterpret_cast<uint4*>(smem);
     for (int i = threadIdx.x; i < (NSER * CROW + NSER * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+    for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
   }
   // the next item: tile, record range, first records, sumfix entry, dirty flag
-  uint32_t item = blockIdx.x;
+  uint32_t item = first;
   uint32_t t = 0, a = 0, e = 0;
   uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
   int64_t f = 0;
@@ -525,7 +541,7 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
       n1 = ld(g + 4u * NT, e);
     }
     if (threadIdx.x < NSER) {
-      const uint32_t s = t * TILE + threadIdx.x;
+      const uint32_t s = t * TILE + half * 16 + threadIdx.x;
       f = 0;
       if (s < st.S) {
         f = st.sumfix[s];
@@ -535,7 +551,7 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
   };
   fetch(item);
   __syncthreads();
-  for (; item < cold_items; item += gridDim.x) {
+  for (; item < cold_items; item += stride) {
     const uint32_t tc = t;
     const bool dc = dirty;
     if (threadIdx.x < NSER) fixl[threadIdx.x] = f;
@@ -550,31 +566,77 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const uint32_t gk = g + (k >> 2) * 4u * NT + (k & 3);
-          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+          x[k] = (gk < a || gk >= e) ? 0xFFFFFFFFu : own(x[k]);
         }
         count_batch<8>(x, lut2, hist_add, sum_add);
       }
     } else if (!(g_dbg & 0x100)) {
       for_tile_records<NT>(segs, tc, 0, plan.tile_tot[tc], [&](uint32_t rec) {
-        const uint32_t x[1] = {rec};
+        const uint32_t x[1] = {own(rec)};
         count_batch<1>(x, lut2, hist_add, sum_add);
       });
     }
     __syncthreads();  // counts complete; fixl visible
-    fetch(item + gridDim.x);
-    const uint32_t s0 = tc * TILE;
+    fetch(item + stride);
+    const uint32_t s0 = tc * TILE + half * 16;
+    // linear emission: a clean whole tile inside the output range of a resetting
+    // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
+    // of 14384 16-B chunks by the whole workgroup in step -- 5.6 TB/s against 4.1 for
+    // per-wave rows (tools/mb_store.hip) -- after the per-series summaries
+    const uint32_t oi0 = s0 - out.first;
+    const bool linear = NSER == 32 && !keep && !dc && out.counts != nullptr && s0 >= out.first &&
+                        oi0 + TILE <= out.count && s0 + TILE <= st.S && (oi0 & 1u) == 0u && !(g_dbg & 0x4000000);
     for (int loc = w; loc < NSER; loc += NT / 64) {
       const uint32_t s = s0 + loc;
+      const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
         const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
-        emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dc, keep, final_mode, st, tb, out);
+        if (linear) {
+          const int ng = lane_groups(lane);
+          uint32_t g[9];
+#pragma unroll
+          for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(SrcLds16{row}.get4(28 * lane + 4 * q)) : 0u;
+          if (!(g_dbg & 0x40000))
+            wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+        } else {
+          emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
+        }
       }
-      // this wave owns the row: clear it for the next item (LDS ops of a wave stay in order)
-      uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
-      for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (!linear) {  // this wave owns the row: clear it for the next item (a wave's LDS ops stay in order)
+        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
+        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
       vsl[loc * 64 + lane] = 0u;
     }
-    if (threadIdx.x == 0) st.dirty[tc] = keep ? 1 : 0;
+    if (linear) {
+      __syncthreads();  // summaries have read the rows
+      // chunk c = flat elements 4c..4c+3 of [32][1798]: two u16 pairs, each an LDS word
+      // read by this chunk only (and cleared here; word 899 of a row is never written)
+      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
+      constexpr int NCH = TILE * NB / 4;
+      for (int c = threadIdx.x; c < NCH; c += NT) {
+        const int e0 = 4 * c;
+        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
+        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
+        // the second pair is the next word (one ds_read2/ds_write2), except for the
+        // chunk that straddles into the next row (b0 = 1796)
+        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
+        uint32_t x, y;
+        if (b0 != NB - 2) {
+          x = p0[0];
+          y = p0[1];
+          p0[0] = 0u;
+          p0[1] = 0u;
+        } else {
+          x = *p0;
+          y = *p1;
+          *p0 = 0u;
+          *p1 = 0u;
+        }
+        if (!(g_dbg & 0x200)) o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+      }
+    }
+    if (threadIdx.x == 0 && half == 0) st.dirty[tc] = keep ? 1 : 0;
     __syncthreads();  // rows cleared, fixl consumed
   }
 }
@@ -812,8 +874,11 @@ hipError_t set_snapshot_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)acc_cold_lds(32));
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold_p<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)acc_cold_lds(32));
+  e = hipFuncSetAttribute((const void*)k_accum_cold_p<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)acc_cold_p_lds(32));
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_cold_p<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)acc_cold_p_lds(16));
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_cold<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)acc_cold_lds(16));
@@ -859,9 +924,15 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
           ncu = 256;
       }
-      const uint32_t grid = cold_items < (uint32_t)ncu ? cold_items : (uint32_t)ncu;
-      hipLaunchKernelGGL((k_accum_cold_p<1024>), dim3(grid), dim3(1024), acc_cold_lds(32), st, segs, plan, state, tb,
-                         out, cold_items, final_mode, reset);
+      if (g_dbg_host & 0x2000000) {  // bit 0x2000000: half-tile items, two 512-thread workgroups per CU
+        const uint32_t pairs = std::min<uint32_t>(cold_items, (uint32_t)ncu);
+        hipLaunchKernelGGL((k_accum_cold_p<16, 512>), dim3(((pairs + 7) / 8) * 16), dim3(512), acc_cold_p_lds(16), st,
+                           segs, plan, state, tb, out, cold_items, final_mode, reset);
+      } else {
+        const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)ncu);
+        hipLaunchKernelGGL((k_accum_cold_p<32, 1024>), dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan,
+                           state, tb, out, cold_items, final_mode, reset);
+      }
     } else if (!(g_dbg_host & 0x20000))
       hipLaunchKernelGGL((k_accum_cold<32, 1024>), dim3(cold_items), dim3(1024), acc_cold_lds(32), st, segs, plan,
                          state, tb, out, cold_items, final_mode, reset);
