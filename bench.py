@@ -92,7 +92,8 @@ def gen_inputs(torch, synth_lib, workload, S, N, rank, stream):
 
 
 # engine timer -> the kernels it brackets (names as in tools/pmc_summary.py)
-PMC_PARTS = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold", "accum_hot"]}
+# (steady state: the accumulate timer brackets the persistent cold kernel and the split kernel)
+PMC_PARTS = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold_p", "accum_split"]}
 
 
 def load_pmc_traffic(path, workload, S, N):
