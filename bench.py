@@ -10,6 +10,11 @@ Default workload (N=1): BASELINE config C3 on one GPU -- 1,000,000 series,
 1e9 samples, Zipf(s=1) series ids, log-normal values (synthetic; BASELINE.md
 §C3).  With --gpus N (torchrun, one rank per GPU) every rank owns its own
 1M-series shard (series-sharded, no collective on the data path): weak scaling.
+--workload c4 (BASELINE config C4, fleet merge): the same 1M series are
+sample-sharded over the ranks (1e9 samples per step in total); each rank ingests
+its shard, exports dense state, the ranks reduce-scatter it over RCCL and each
+summarizes its series slice (strong scaling; collective time and bus GB/s are
+reported under "merge").
 
 Prints ONE JSON line (rank 0).  `value` = samples/s over all ranks;
 `roofline` = the dominant kernel's algorithmic bytes / its average duration
@@ -45,7 +50,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["c3", "c2", "c1"], default="c3")
+    p.add_argument("--workload", choices=["c3", "c2", "c1", "c4"], default="c3")
     p.add_argument("--series", type=int, default=None, help="series per rank (default: workload's)")
     p.add_argument("--samples", type=int, default=None, help="samples per rank per step (default: workload's)")
     p.add_argument("--bin-mode", type=int, default=0)
@@ -61,6 +66,8 @@ def parse():
 def workload_defaults(args):
     if args.workload == "c3":
         S, N = 1_000_000, 1_000_000_000
+    elif args.workload == "c4":  # N = this rank's share of the 1e9 samples
+        S, N = 1_000_000, 1_000_000_000 // int(os.environ.get("WORLD_SIZE", "1"))
     elif args.workload == "c2":
         S, N = 100_000, 100_000_000
     else:
@@ -74,12 +81,13 @@ def gen_inputs(torch, synth_lib, workload, S, N, rank, stream):
     values = torch.empty(N, dtype=torch.float32, device=dev)
     sp = ctypes.c_void_p(series.data_ptr())
     vp = ctypes.c_void_p(values.data_ptr())
-    if workload == "c3":
+    if workload in ("c3", "c4"):
         from linkerd_amd import synth
         cdf = torch.from_numpy(synth.zipf_cdf(S)).to(dev)
+        # c3: every rank its own series shard; c4: one series space, rank r draws samples [r N, (r+1) N)
         rc = synth_lib.l5ds_gen_zipf(sp, vp, ctypes.c_uint64(N), ctypes.c_uint64(S), ctypes.c_void_p(cdf.data_ptr()),
                                      ctypes.c_uint64(3), ctypes.c_double(0.8), ctypes.c_uint64(rank * N),
-                                     ctypes.c_uint32(rank * S), ctypes.c_void_p(stream))
+                                     ctypes.c_uint32(rank * S if workload == "c3" else 0), ctypes.c_void_p(stream))
     elif workload == "c2":
         K = N // S
         rc = synth_lib.l5ds_gen_c2(sp, vp, ctypes.c_uint64(S), ctypes.c_uint64(K), ctypes.c_uint64(2),
@@ -123,7 +131,7 @@ def cpu_baseline(workload, S, N, sample, threads):
     from linkerd_amd import synth
     from oracle import oracle as O
     n = min(sample, N)
-    if workload == "c3":
+    if workload in ("c3", "c4"):
         s, v = synth.c3(S=S, N=n)
     elif workload == "c2":
         s, v = synth.c2(S=S, K=max(1, n // S))
@@ -183,12 +191,31 @@ def main():
         eng.set_param(N_.PARAM_DIRECT_DIV, args.direct_div)
     if args.split_min is not None:
         eng.set_param(N_.PARAM_SPLIT_MIN, args.split_min)
+    fleet = args.workload == "c4"
     summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
     counts = torch.empty((S, N_.NBUCKETS), dtype=torch.int32, device=dev)
+    totals = torch.empty(S, dtype=torch.int64, device=dev)
+    merged = {}
+    merge_ev = []
 
     def step():
         eng.ingest(series, values)
-        eng.snapshot_into(summ, counts, reset=True)
+        if not fleet:
+            eng.snapshot_into(summ, counts, reset=True)
+            return
+        # C4: dense partial state -> reduce-scatter (RCCL) -> summaries of this rank's slice
+        eng.export_state(counts=counts, totals=totals, reset=True)
+        if merge_ev:
+            merge_ev[0].record()
+        if distributed:
+            from linkerd_amd.fleet import fleet_merge
+            c, t, first = fleet_merge(counts, totals, mode="reduce_scatter")
+        else:
+            c, t, first = counts, totals, 0
+        if merge_ev:
+            merge_ev[1].record()
+        eng.summarize_dense(c, t, out=summ[:c.shape[0]])
+        merged.update(c=c, n=c.shape[0])
 
     def barrier():
         if distributed:
@@ -212,10 +239,32 @@ def main():
         elapsed = float(t.item())
 
     # sanity: every sample landed in exactly one bucket of the last snapshot
-    got = int(counts.sum(dtype=torch.int64).item())
+    if fleet:
+        tot = torch.stack([merged["c"].sum(dtype=torch.int64), summ[:merged["n"], 0].sum()])
+        if distributed:
+            dist.all_reduce(tot)
+        want = N * world
+    else:
+        tot = torch.stack([counts.sum(dtype=torch.int64), summ[:, 0].sum()])
+        want = N
     if not os.environ.get("L5DH_DBG"):  # L5DH_DBG selects timing-only kernel variants
-        assert got == N, f"bucket counts sum {got} != {N}"
-        assert int(summ[:, 0].sum().item()) == N
+        assert int(tot[0].item()) == want, f"bucket counts sum {int(tot[0].item())} != {want}"
+        assert int(tot[1].item()) == want
+
+    merge = None
+    if fleet:  # collective time alone (events around the reduce-scatter, separate steps)
+        merge_ev[:] = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        ms = []
+        for _ in range(3):
+            step()
+            torch.cuda.synchronize()
+            ms.append(merge_ev[0].elapsed_time(merge_ev[1]))
+        merge_ev.clear()
+        cms = sorted(ms)[1]
+        nbytes = S * (N_.NBUCKETS * 4 + 8)  # int32 counts + int64 total per series, per rank
+        merge = {"collective": "reduce_scatter (RCCL)" if distributed else "none (1 rank)",
+                 "collective_ms": round(cms, 4), "bytes_per_rank": nbytes,
+                 "bus_GBs": round(nbytes * (world - 1) / world / (cms * 1e-3) / 1e9, 1) if world > 1 else None}
 
     # per-kernel device time (HIP events on the engine's stream), separate steps
     eng.set_param(N_.PARAM_TIMING, 1)
@@ -229,7 +278,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_samples = N * world
     value = total_samples * args.steps / elapsed
-    balg = 8 * N + 7280 * S
+    balg = 8 * N + 7280 * S if not fleet else 8 * N + 7280 * S // world  # c4: a rank writes its slice
     kernels = {}
     for name, (ms, launches) in kt.items():
         if launches == 0:
@@ -259,12 +308,14 @@ def main():
         line = {
             "metric": "histogram samples ingested+summarized/sec (1M series) and % HBM peak",
             "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong" if fleet else "weak", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic",
             "config": {"workload": {"c3": "C3: 1M series x 1e9 samples, Zipf(s=1) ids, log-normal values",
                                     "c2": "C2: 100k series x 1k samples, permuted COO",
-                                    "c1": "C1: 1 series x 1e7 log-normal samples"}[args.workload],
-                       "series_per_gpu": S, "samples_per_gpu_per_step": N, "parallelism": f"series-sharded x{world}",
+                                    "c1": "C1: 1 series x 1e7 log-normal samples",
+                                    "c4": "C4: fleet merge, 1M series, 1e9 Zipf(s=1) samples per step "
+                                          "sample-sharded over the ranks, reduce-scatter of dense counts"}[args.workload],
+                       "series_per_gpu": S, "samples_per_gpu_per_step": N, "parallelism": f"{'sample-sharded' if fleet else 'series-sharded'} x{world}",
                        "step": "ingest (count+scan+bin1+bin2) + snapshot(reset, dense counts + summaries)"},
             "roofline": roofline,
             "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -273,6 +324,8 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
         }
+        if merge:
+            line["merge"] = merge
         print(json.dumps(line), flush=True)
     eng.close()
     if distributed:

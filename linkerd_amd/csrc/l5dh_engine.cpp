@@ -395,7 +395,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
 }
 
 int fold(l5dh_ctx* c) {
-  Outputs none{nullptr, nullptr, 0, 0};
+  Outputs none{nullptr, nullptr, 0, 0, nullptr};
   return aggregate(c, 0, 0, none);
 }
 
@@ -517,7 +517,7 @@ int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, 
       d_counts = static_cast<int32_t*>(c->stage_counts.p);
     }
   }
-  Outputs o{d_summ, d_counts, first, count};
+  Outputs o{d_summ, d_counts, first, count, nullptr};
   if (full_range(c, first, count)) {
     if ((r = aggregate(c, 1, reset, o))) return r;
   } else {
@@ -692,7 +692,8 @@ int l5dh_export_state(l5dh_ctx* c, uint32_t first, uint32_t count, int32_t* coun
   if ((uint64_t)first + count > c->S) return fail(c, -EINVAL, "series range out of bounds");
   if (count == 0) return 0;
   int r;
-  if ((r = fold(c))) return r;
+  const bool fused = full_range(c, first, count) && reset;  // the fleet merge's export: one aggregate pass
+  if (!fused && (r = fold(c))) return r;
   const bool cnt_dev = counts && is_device_ptr(counts) && ((uintptr_t)counts % 8 == 0);
   const bool tot_dev = totals && is_device_ptr(totals) && ((uintptr_t)totals % 8 == 0);
   int32_t* d_counts = nullptr;
@@ -713,8 +714,12 @@ int l5dh_export_state(l5dh_ctx* c, uint32_t first, uint32_t count, int32_t* coun
       d_totals = static_cast<int64_t*>(c->stage_totals.p);
     }
   }
-  Outputs o{nullptr, d_counts, first, count};
-  {
+  if (fused) {
+    // pending records and state go straight into the caller's dense rows and
+    // totals (no fold into state, no second pass), and the state is left clean
+    if ((r = aggregate(c, 1, 1, Outputs{nullptr, d_counts, first, count, d_totals}))) return r;
+  } else {
+    Outputs o{nullptr, d_counts, first, count, nullptr};
     KTimer kt(c, L5DH_K_HOT);
     HIPCHK(c, launch_rows(state(c), nullptr, nullptr, tables(c), o, reset, d_totals, c->stream));
   }
@@ -751,7 +756,7 @@ int l5dh_summarize_dense(l5dh_ctx* c, const int32_t* counts, const int64_t* tota
     if ((r = ensure(c, c->stage_summ, n * 88))) return r;
     d_summ = static_cast<Summary88*>(c->stage_summ.p);
   }
-  Outputs o{d_summ, nullptr, 0, (uint32_t)n};
+  Outputs o{d_summ, nullptr, 0, (uint32_t)n, nullptr};
   {
     KTimer kt(c, L5DH_K_HOT);
     HIPCHK(c, launch_rows(state(c), d_counts, d_totals, tables(c), o, 0, nullptr, c->stream));

@@ -14,6 +14,12 @@
 #include <algorithm>
 
 #include "l5dh_device.hpp"
+// L5DH_EXP (compile time, tools/mk_var.sh): timing-only variants, results invalid.
+//   4 k_count without hot-column aggregation, 8 k_count loads only,
+//   16 k_bin1 loads + ranking only (no scan, scatter or run writes)
+#ifndef L5DH_EXP
+#define L5DH_EXP 0
+#endif
 
 namespace l5dh {
 namespace {
@@ -49,7 +55,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
   const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot columns of the previous batch (aggregation only)
-  const uint32_t hk[2] = {hot0 < C ? hot0 : 0xFFFFFFFFu, hot1 < C ? hot1 : 0xFFFFFFFFu};
+  const uint32_t hk[2] = {hot0 < C && !(L5DH_EXP & 4) ? hot0 : 0xFFFFFFFFu, hot1 < C && !(L5DH_EXP & 4) ? hot1 : 0xFFFFFFFFu};
   bool bad = false;
   if (lo < hi) {
     size_t done = lo;
@@ -60,6 +66,10 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const size_t wlast = threadIdx.x | 63;  // last lane of this wave: uniform loop bound
       for (; wlast - threadIdx.x + i + 3 * WG < nv; i += 4 * WG) {
         const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
+        if (L5DH_EXP & 8) {  // timing: loads only
+          asm volatile("" ::"v"(a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w));
+          continue;
+        }
         const uint32_t sv[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
         uint2 wv[16];
 #pragma unroll
@@ -421,6 +431,16 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
+    }
+    if (L5DH_EXP & 16) {  // timing: loads + ranking only (no scan, scatter or run writes)
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < PT; ++k) x ^= pk[k] ^ rec[k];
+      if (x == 0x12345678u) out1[threadIdx.x] = x;
+      __syncthreads();
+      for (uint32_t j = threadIdx.x; j <= TB; j += NT) cnt[j] = 0;
+      __syncthreads();
+      continue;
     }
     __syncthreads();
     if (wv == 0) {  // one wave: hot-slot lane prefixes and totals, then the bin scan (DPP, no barriers)

@@ -102,6 +102,7 @@ struct Outputs {
   Summary88* summ;         // nullable, index = series - first
   int32_t* counts;         // nullable, [count][1798]
   uint32_t first, count;
+  int64_t* totals;         // nullable, [count] exact sums (the fleet-merge export)
 };
 
 // ---- launchers (all enqueue on `st`) ----

@@ -9,6 +9,11 @@
 //   k_hot_finish summaries of hot tiles from their merged state rows
 //   k_rows       summaries / dense copies of state rows or external rows
 #include "l5dh_device.hpp"
+// L5DH_EXP (compile time, tools/mk_var.sh): timing-only variants, results invalid.
+//   1 k_accum_split without the value-sum atomics, 2 without the bin atomics
+#ifndef L5DH_EXP
+#define L5DH_EXP 0
+#endif
 
 namespace l5dh {
 namespace {
@@ -278,6 +283,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   int64_t total = (int64_t)vsum + fix;  // fix = sumfix[s], read (and cleared) by the caller
   if (dirty) total += st.total[s];
   if (lane == 0 && keep) st.total[s] = total;
+  if (lane == 0 && emit && out.totals) out.totals[oi] = total;
   if (emit && !(g_dbg & 0x40000)) {  // 0x40000 (timing): no summaries
     Summary88* so = out.summ ? out.summ + oi : nullptr;
     if (dirty)
@@ -598,6 +604,7 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
           for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(SrcLds16{row}.get4(28 * lane + 4 * q)) : 0u;
           if (!(g_dbg & 0x40000))
             wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          if (lane == 0 && out.totals) out.totals[s - out.first] = (int64_t)vsum + fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
         }
@@ -761,8 +768,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
         if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
       }
       count_batch<8>(
-          x, lut2, [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-          [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
+          x, lut2, [&](uint32_t loc, uint32_t b) { if (!(L5DH_EXP & 2)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
+          [&](uint32_t loc, uint32_t v) { if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
     }
   }
   __syncthreads();
@@ -804,6 +811,7 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
         uint32_t g[9];
         row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
         wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+        if (lane == 0 && out.totals) out.totals[oi] = total;
       }
     }
     if (lane == 0) {
