@@ -64,8 +64,27 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       const uint4* __restrict__ p = reinterpret_cast<const uint4*>(series + lo);
       size_t i = threadIdx.x;
       const size_t wlast = threadIdx.x | 63;  // last lane of this wave: uniform loop bound
-      for (; wlast - threadIdx.x + i + 3 * WG < nv; i += 4 * WG) {
-        const uint4 a = p[i], b = p[i + WG], c = p[i + 2 * WG], d = p[i + 3 * WG];
+      // software-pipelined: the next two groups of 4 x 16 B per thread are in flight
+      // during this one's LDS counting, so the HBM stream does not pause behind it
+      auto full = [&](size_t j) { return wlast - threadIdx.x + j + 3 * WG < nv; };
+      auto load4 = [&](size_t j, uint4 (&x)[4]) {
+        if (full(j)) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = p[j + q * WG];
+        }
+      };
+      uint4 n0[4], n1[4];
+      load4(i, n0);
+      if (!(L5DH_EXP & 128)) load4(i + 4 * WG, n1);
+      for (; full(i); i += 4 * WG) {
+        const uint4 a = n0[0], b = n0[1], c = n0[2], d = n0[3];
+        if (!(L5DH_EXP & 128)) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) n0[q] = n1[q];
+          load4(i + 8 * WG, n1);
+        } else {
+          load4(i + 4 * WG, n0);
+        }
         if (L5DH_EXP & 8) {  // timing: loads only
           asm volatile("" ::"v"(a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w));
           continue;
