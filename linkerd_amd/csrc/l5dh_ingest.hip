@@ -16,7 +16,9 @@
 #include "l5dh_device.hpp"
 // L5DH_EXP (compile time, tools/mk_var.sh): timing-only variants, results invalid.
 //   4 k_count without hot-column aggregation, 8 k_count loads only,
-//   16 k_bin1 loads + ranking only (no scan, scatter or run writes)
+//   16 k_bin1 loads + ranking only (no scan, scatter or run writes),
+//   1024 k_bin1 run writes replaced by the same number of sequential stores,
+//   2048 ... by whole 64-B segments in 1024 interleaved sequential streams
 #ifndef L5DH_EXP
 #define L5DH_EXP 0
 #endif
@@ -510,7 +512,15 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 #pragma unroll
     for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
       const uint2 e = stage[threadIdx.x + k * NT];
-      if (!(dbg & 1)) ((e.y >> 31) ? records : out1)[e.y & 0x7FFFFFFFu] = e.x;
+      if (L5DH_EXP & 1024)  // timing: the same stores, sequential (where the slots were read)
+        out1[c0 + threadIdx.x + k * NT] = e.x;
+      else if (L5DH_EXP & 2048) {  // timing: whole 64-B segments, 1024 interleaved sequential streams
+        const size_t idx = c0 + threadIdx.x + k * NT;
+        const size_t seg = idx >> 4, nseg = n >> 4;
+        out1[((seg & 1023) * (nseg >> 10) + (seg >> 10)) * 16 + (idx & 15)] = e.x;
+      }
+      else if (!(dbg & 1))
+        ((e.y >> 31) ? records : out1)[e.y & 0x7FFFFFFFu] = e.x;
     }
     __syncthreads();
   }
