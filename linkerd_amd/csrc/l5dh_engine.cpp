@@ -465,6 +465,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
       HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
                               (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
+                              ((c->dbg >> 20) & 1) || ((c->dbg >> 22) & 1),  // k_bin1 variants with hot slots
                               c->stream));
       c->split_cur ^= 1;
     }

@@ -540,7 +540,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
                                                  uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
                                                  uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax,
-                                                 uint32_t split_min) {
+                                                 uint32_t split_min, int hot_bins) {
   __shared__ uint32_t lds[17];
   __shared__ unsigned long long best[16];
   __shared__ uint32_t lhd[33], lhs[33];
@@ -667,22 +667,22 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       plan[PLAN_DBITS + 2 * j + 1] = d1;
       plan[PLAN_DPRE + 2 * j + 1] = de + (uint32_t)__popc(d0);
     }
+    // (stores only: the half totals of the direct tiles are read below, one direct tile
+    // per thread, instead of as a chain of dependent loads in this loop)
     uint32_t di = de;
     for (int q = 0; q < 2; ++q) {
       uint32_t w = q ? d1 : d0;
       const uint32_t cw = q ? c1 : c0;
+      const uint32_t sp = cur[SPLIT_PRE + 2 * j + q];
       while (w) {
         const uint32_t b = (uint32_t)(__ffs((int)w) - 1);
         w &= w - 1u;
-        const uint32_t si = cur[SPLIT_PRE + 2 * j + q] + (uint32_t)__popc(cw & ((1u << b) - 1u));
         plan[PLAN_DLIST + di] = j * ST_TILES + 32u * q + b;
-        plan[PLAN_DSI + di] = si;
-        push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * di));
-        push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * di + 1));
+        plan[PLAN_DSI + di] = sp + (uint32_t)__popc(cw & ((1u << b) - 1u));
         ++di;
       }
     }
-    if (ctot) push((ctot << 11) | j);
+    if (ctot && hot_bins) push((ctot << 11) | j);
     // the next batch's split set
     nxt[SPLIT_BITS + 2 * j] = n0;
     nxt[SPLIT_PRE + 2 * j] = ne;
@@ -705,6 +705,12 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     plan[PLAN_ND] = ndtot;
     nxt[0] = nnt;
   }
+  __syncthreads();  // the direct list is written
+  for (uint32_t d = threadIdx.x; hot_bins && d < ndtot; d += 1024) {  // the direct tiles' half bins as hot-bin candidates
+    const uint32_t si = plan[PLAN_DSI + d];
+    push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * d));
+    push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * d + 1));
+  }
   // grand total, the hot bins and the two biggest tiles (block reductions)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   auto block_reduce = [&](unsigned long long v, bool is_max) -> unsigned long long {
@@ -721,16 +727,19 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
     return r;
   };
   const unsigned long long grand = block_reduce(tot, false);
-  unsigned long long ks[NHOT];
+  // (only the lane-private hot-slot variants of k_bin1 use them: 16 barriers saved otherwise)
+  unsigned long long ks[NHOT] = {};
   int head = 0;  // this thread's first bin not yet selected
+  if (hot_bins) {
 #pragma unroll
-  for (int q = 0; q < NHOT; ++q) {
-    unsigned long long mine = 0;
+    for (int q = 0; q < NHOT; ++q) {
+      unsigned long long mine = 0;
 #pragma unroll
-    for (int r = 0; r < NHOT; ++r)
-      if (r == head) mine = bk[r];
-    ks[q] = block_reduce(mine, true);
-    if (mine != 0 && mine == ks[q]) ++head;
+      for (int r = 0; r < NHOT; ++r)
+        if (r == head) mine = bk[r];
+      ks[q] = block_reduce(mine, true);
+      if (mine != 0 && mine == ks[q]) ++head;
+    }
   }
   const unsigned long long t1 = block_reduce(tkA, true);
   const unsigned long long t2 = block_reduce(tkA == t1 ? tkB : tkA, true);
@@ -979,11 +988,12 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
 }
 
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
-                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, hipStream_t st) {
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, int hot_bins,
+                         hipStream_t st) {
   const uint32_t FS = (F + 63) / 64;
   const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
   hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap),
-                     split_min);
+                     split_min, hot_bins);
   return hipGetLastError();
 }
 

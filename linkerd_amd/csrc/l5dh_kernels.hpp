@@ -144,7 +144,8 @@ constexpr int PLAN_WORDS = PLAN_SPLIT + 2 * SPLIT_SLOT;
 // 2^k), k the smallest power keeping <= dmax tiles.  The next batch's split set
 // `nxt`: the tiles with records >= max(split_min, 2^k) (<= SPLIT_MAX tiles).
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
-                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, hipStream_t st);
+                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, int hot_bins,
+                         hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
                        const uint32_t* coltot, const uint32_t* split, uint32_t* scratch1, uint32_t* records,
