@@ -184,7 +184,7 @@ struct l5dh_ctx {
   int split_cur = 0;              // split-set slot of the next batch in d_b2plan + PLAN_SPLIT
   uint32_t* d_header = nullptr;
   uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
-  uint32_t* h_header = nullptr;  // pinned
+  uint32_t* h_header = nullptr;  // pinned: [0..3] plan header, [4] ingest error flag
   int G_max = 256;
   // segments
   struct Seg {
@@ -399,10 +399,13 @@ int fold(l5dh_ctx* c) {
   return aggregate(c, 0, 0, none);
 }
 
+// The ingest error flag comes back through pinned memory with the stream's one
+// synchronization (h_header[4]; a pageable copy would add a second round trip).
 int check_err(l5dh_ctx* c) {
-  uint32_t e = 0;
-  HIPCHK(c, hipMemcpyAsync(&e, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  int r = sync_stream(c);
+  if (r) return r;
+  const uint32_t e = c->h_header[4];
   if (e) {
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
     return fail(c, -EINVAL, "series id >= max_series in ingest batch (samples dropped)");
@@ -485,9 +488,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   sg.n = n;
   c->nseg++;
-  // No caller pointer is retained past return: wait for the batch to be binned.
-  int r = sync_stream(c);
-  if (r) return r;
+  // No caller pointer is retained past return: wait for the batch to be binned
+  // (the same synchronization brings the error flag back).
   return check_err(c);
 }
 
@@ -602,7 +604,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
   }
-  if (hipHostMalloc((void**)&c->h_header, 16, 0) != hipSuccess) return bail(-ENOMEM);
+  if (hipHostMalloc((void**)&c->h_header, 32, 0) != hipSuccess) return bail(-ENOMEM);  // header[4] + err flag
   // constant tables
   int32_t lim_pad[LIM_PAD], mid[NB], base[ROW] = {0};
   for (int i = 0; i < LIM_PAD; ++i) lim_pad[i] = i < NL ? hl.L[i] : INT_MAXV;
@@ -803,9 +805,7 @@ int l5dh_sync(l5dh_ctx* c) {
   if (!c) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  int r = sync_stream(c);
-  if (r) return r;
-  return check_err(c);
+  return check_err(c);  // synchronizes the stream
 }
 
 int l5dh_set_stream(l5dh_ctx* c, void* s) {
