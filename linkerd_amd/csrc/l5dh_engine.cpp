@@ -185,6 +185,7 @@ struct l5dh_ctx {
   uint32_t* d_header = nullptr;
   uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
   uint32_t* h_header = nullptr;  // pinned: [0..3] plan header, [4] ingest error flag
+  uint32_t* h_header_dev = nullptr;  // its device-side address (the plan kernel writes the header there)
   int G_max = 256;
   // segments
   struct Seg {
@@ -321,7 +322,7 @@ State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c-
 
 Plan plan(l5dh_ctx* c) {
   return Plan{c->d_tile_tot,   c->d_cold_tile,   static_cast<uint32_t*>(c->hot_item.p), static_cast<uint2*>(c->split_item.p),
-              c->d_hot_list, c->d_tile_flags, c->d_header};
+              c->d_hot_list, c->d_tile_flags, c->d_header, c->h_header_dev};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -352,8 +353,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, c->d_dirty, pl, c->stream));
   }
-  HIPCHK(c, hipMemcpyAsync(c->h_header, c->d_header, 16, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the plan kernel wrote h_header (mapped pinned memory)
   const uint32_t cold_items = c->h_header[0];
   const uint32_t hot = c->h_header[1];
   const uint32_t hot_items = c->h_header[2];
@@ -604,7 +604,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
   }
-  if (hipHostMalloc((void**)&c->h_header, 32, 0) != hipSuccess) return bail(-ENOMEM);  // header[4] + err flag
+  if (hipHostMalloc((void**)&c->h_header, 32, hipHostMallocMapped) != hipSuccess) return bail(-ENOMEM);  // header[4] + err flag
+  if (hipHostGetDevicePointer((void**)&c->h_header_dev, c->h_header, 0) != hipSuccess) return bail(-ENOMEM);
   // constant tables
   int32_t lim_pad[LIM_PAD], mid[NB], base[ROW] = {0};
   for (int i = 0; i < LIM_PAD; ++i) lim_pad[i] = i < NL ? hl.L[i] : INT_MAXV;

@@ -96,6 +96,7 @@ struct Plan {
   uint32_t* hot_list;      // [F] big tiles
   uint8_t* tile_flags;     // [F] TF_*
   uint32_t* header;        // [4] cold items, big tiles, mixed-half items, split items
+  uint32_t* header_host;   // [4] the same, written by the plan kernel into pinned host memory
 };
 
 struct Outputs {

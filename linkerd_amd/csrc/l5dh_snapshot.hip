@@ -94,10 +94,11 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
     plan.tile_flags[t] = flags;
   }
   if (threadIdx.x == 0) {
-    plan.header[0] = tot_c;
-    plan.header[1] = tot_hot;
-    plan.header[2] = tot_h;
-    plan.header[3] = tot_s;
+    const uint32_t h[4] = {tot_c, tot_hot, tot_h, tot_s};
+    for (int k = 0; k < 4; ++k) {
+      plan.header[k] = h[k];
+      plan.header_host[k] = h[k];
+    }
   }
 }
 
@@ -174,7 +175,10 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
     if (blockIdx.x == 0) block_excl_scan<1024>(y, lds[k], &ty);
     if (threadIdx.x == 0) {
       base[k] = tx;
-      if (blockIdx.x == 0) plan.header[k] = ty;  // header: cold items, big tiles, mixed-half items, split items
+      if (blockIdx.x == 0) {  // header: cold items, big tiles, mixed-half items, split items
+        plan.header[k] = ty;
+        plan.header_host[k] = ty;  // read by the host after the stream sync (no copy to enqueue)
+      }
     }
   }
   __syncthreads();
