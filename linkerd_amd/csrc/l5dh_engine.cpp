@@ -472,6 +472,10 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
                               c->stream));
       c->split_cur ^= 1;
     }
+    if (getenv("L5DH_PRINT_ADDRS"))  // development: buffer placement
+      fprintf(stderr, "l5dh addrs: in %p %p scratch1 %p recs %p table %p (recs-scratch1 = %lld)\n", (const void*)ds,
+              (const void*)dv, c->scratch1.p, sg.recs.p, (void*)c->d_table,
+              (long long)((char*)sg.recs.p - (char*)c->scratch1.p));
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
