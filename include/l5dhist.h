@@ -81,7 +81,7 @@ enum {
   L5DH_K_ACCUM = 3,  /* LDS-private tile histograms + fused summary / dense flush */
   L5DH_K_HOT = 4,    /* split-tile init/finish and row summaries */
   L5DH_K_COPY = 5,   /* H2D/D2H staging copies */
-  L5DH_K_BIN2 = 6,   /* level-2 partition + bucketize (LUT-bracketed search) */
+  L5DH_K_BIN2 = 6,   /* level-2 partition (super-tile runs -> per-tile segments) */
   L5DH_K_NKERNELS = 7
 };
 

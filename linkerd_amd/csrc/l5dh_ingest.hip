@@ -4,7 +4,7 @@
 //   k_colscan  per tile, exclusive prefix over slabs (in place) + tile totals
 //   k_tilescan exclusive prefix over tiles -> tile_base[F+1] (final layout)
 //   k_bin1     level 1: slab -> super-tiles (64 tiles) and direct tiles, LDS
-//              counting sort of 6K-sample sub-chunks, run writes
+//              counting sort of 16K-sample sub-chunks, run writes
 //   k_bin2     level 2: (super-tile, slab block) -> per-(slab, tile) segments
 //   k_bin      single-level alternative (direct scatter)
 //
