@@ -583,7 +583,11 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   if (hipSetDevice(dev) != hipSuccess) return bail(-EIO);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->num_cu = prop.multiProcessorCount;
-  c->G_max = std::max(1, std::min(2 * c->num_cu, 512));
+  // one slab per CU: the count and level-1 kernels hold one 1024-thread workgroup per
+  // CU (LDS-bound), so a second round of slabs only adds table rows (measured: 2 x CUs
+  // is ~1.4 % slower on C2 and no faster on C3)
+  c->G_max = std::max(1, std::min(c->num_cu, 512));
+  if (const char* g = getenv("L5DH_GMAX")) c->G_max = std::max(1, std::min(atoi(g), 512));  // development: slab count
   if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
   if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
