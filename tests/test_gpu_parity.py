@@ -294,3 +294,24 @@ def test_zipf_series_space_1m(oracle, bin_mode):
     touched = np.unique(series)
     np.testing.assert_array_equal(counts[touched], want_counts[touched])
     assert counts.sum() == series.size
+
+
+@pytest.mark.parametrize("gmax", [1, 3, 7, 512])
+def test_slab_counts_bitexact(oracle, monkeypatch, gmax):
+    """Ingest with G = min(L5DH_GMAX, n / 8192) slabs (default: one per CU): the
+    per-(slab, column) prefixes, level-1 cursors and level-2 slab ranges must place
+    every record exactly for any slab count, including one slab and odd counts.
+    Two Zipf batches, so the second runs with split and direct tiles."""
+    monkeypatch.setenv("L5DH_GMAX", str(gmax))
+    rng = np.random.default_rng(100 + gmax)
+    S, n = 5000, 1_500_000
+    eng = _engine(S, 2)
+    o = oracle.OracleHistograms(S)
+    for _ in range(2):
+        series = ((rng.zipf(1.2, size=n) - 1) % S).astype(np.uint32)
+        vals = np.exp(np.log(20.0) + rng.standard_normal(n)).astype(np.float32)
+        eng.ingest(series, vals)
+        o.ingest(series, vals)
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(reset=True), f"gmax={gmax}")
