@@ -22,6 +22,11 @@
 #ifndef L5DH_EXP
 #define L5DH_EXP 0
 #endif
+// hot count columns aggregated by ballot in k_count (2 or 4; the plan holds 4 hints)
+#ifndef L5DH_HK
+#define L5DH_HK 2
+#endif
+static_assert(L5DH_HK >= 2 && L5DH_HK <= 4, "k_count's tail path uses two hot columns; the plan holds four");
 
 namespace l5dh {
 namespace {
@@ -56,8 +61,9 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
-  const uint32_t hot0 = hint[0], hot1 = hint[1];  // hot columns of the previous batch (aggregation only)
-  const uint32_t hk[2] = {hot0 < C && !(L5DH_EXP & 4) ? hot0 : 0xFFFFFFFFu, hot1 < C && !(L5DH_EXP & 4) ? hot1 : 0xFFFFFFFFu};
+  uint32_t hk[L5DH_HK];  // hot columns of the previous batch (aggregation only)
+#pragma unroll
+  for (int h = 0; h < L5DH_HK; ++h) hk[h] = hint[h] < C && !(L5DH_EXP & 4) ? hint[h] : 0xFFFFFFFFu;
   bool bad = false;
   if (lo < hi) {
     size_t done = lo;
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
           bad |= !ok;
           key[k] = ok ? count_key(sv[k], F, wv[k]) : 0xFFFFFFFFu;
         }
-        hot_inc_batch<2, 16>(cnt, key, hk);
+        hot_inc_batch<L5DH_HK, 16>(cnt, key, hk);
       }
       for (; i - threadIdx.x < nv; i += WG) {  // convergent: out-of-range lanes pass invalid ids
         uint4 a = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
@@ -750,11 +756,11 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       plan[3 * FS + 1 + h] = (v > 0 && v * 128 >= grand) ? (uint32_t)(ks[h] & 2047u) : NOKEY;
     }
     // next batch's k_count hints: the count columns of the two biggest tiles
-    // (both halves of the biggest one when it will be split); aggregation only
-    uint32_t hkey[2] = {NOKEY, NOKEY};
+    // (both halves of a tile that will be split); aggregation only
+    uint32_t hkey[4] = {NOKEY, NOKEY, NOKEY, NOKEY};
     int nh = 0;
     const unsigned long long ts[2] = {t1, t2};
-    for (int q = 0; q < 2 && nh < 2; ++q) {
+    for (int q = 0; q < 2 && nh < 4; ++q) {
       const uint64_t v = ts[q] >> 16;
       if (v == 0 || v * 64 < grand) continue;
       const uint32_t t = (uint32_t)(ts[q] & 0xFFFFu);
@@ -763,13 +769,12 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       if (wd & bit) {
         const uint32_t si = nxt[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
         hkey[nh++] = F + 2 * si;
-        if (nh < 2) hkey[nh++] = F + 2 * si + 1;
+        hkey[nh++] = F + 2 * si + 1;
       } else {
         hkey[nh++] = t;
       }
     }
-    plan[PLAN_HINT] = hkey[0];
-    plan[PLAN_HINT + 1] = hkey[1];
+    for (int h = 0; h < 4; ++h) plan[PLAN_HINT + h] = hkey[h];
   }
 }
 

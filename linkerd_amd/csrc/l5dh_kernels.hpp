@@ -132,7 +132,7 @@ constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + 2 x direct tiles +
 constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4; }
 constexpr size_t BIN1_SCRATCH_PAD = 16384 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
-constexpr int PLAN_HINT = 2040;     // [2] hot count-table columns: hints for the next batch's k_count
+constexpr int PLAN_HINT = 2040;     // [4] hot count-table columns: hints for the next batch's k_count
 constexpr int PLAN_DBITS = 2048;    // [1024] direct-tile bitmap of this batch (bit t of word t/32)
 constexpr int PLAN_DPRE = 3072;     // [1024] direct tiles before word w
 constexpr int PLAN_DLIST = 4096;    // [256] direct tile ids, ascending
