@@ -517,7 +517,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       for (uint32_t i = threadIdx.x; i < NHOT * 64; i += NT) hcnt[i] = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
-      const uint2 e = stage[threadIdx.x + k * NT];
+      const uint2 e = stage[(uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane];  // each wave: a contiguous PT x 64 range
       if (L5DH_EXP & 1024)  // timing: the same stores, sequential (where the slots were read)
         out1[c0 + threadIdx.x + k * NT] = e.x;
       else if (L5DH_EXP & 2048) {  // timing: whole 64-B segments, 1024 interleaved sequential streams
