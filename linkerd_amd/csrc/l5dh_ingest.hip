@@ -916,11 +916,12 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
     __syncthreads();
     {
       uint2 ev[PT];
+      const uint32_t w0 = (threadIdx.x >> 6) * (PT * 64) + (threadIdx.x & 63u);  // each wave: a contiguous PT x 64 range
 #pragma unroll
-      for (int k = 0; k < PT; ++k) ev[k] = stage[threadIdx.x + k * B2_NT];
+      for (int k = 0; k < PT; ++k) ev[k] = stage[w0 + k * 64];
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        const uint32_t i = threadIdx.x + k * B2_NT;
+        const uint32_t i = w0 + k * 64;
         if (i < total) records[ev[k].y + i] = ev[k].x;
       }
     }
