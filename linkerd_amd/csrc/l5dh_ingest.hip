@@ -35,7 +35,10 @@ constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
-constexpr uint32_t B2_ITEM = 32768;  // target level-1 records per k_bin2 item
+#ifndef L5DH_B2_ITEM
+#define L5DH_B2_ITEM 32768
+#endif
+constexpr uint32_t B2_ITEM = L5DH_B2_ITEM;  // target level-1 records per k_bin2 item
 
 // ------------------------------------------------------------------------
 // Count key of a valid sample: its tile, or for a split tile the column of its
