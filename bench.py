@@ -1,26 +1,35 @@
 """Benchmark of the histogram hot path (BASELINE.json metric).
 
-One step = one snapshot interval of the reference's Metric.Stat path: ingest the
-whole batch of (series u32, value f32) samples already resident in HBM
-(Metric.Stat.add, batched) and snapshot + reset every series into dense int32
-bucket counts and 88-byte HistogramSummary records (snapshotHistograms,
-AdminMetricsExportTelemeter.scala:154-162).
+One step = one snapshot interval of the reference's Metric.Stat path: ingest a
+batch of (series u32, value f32) samples already resident in HBM (Metric.Stat.add,
+batched) and snapshot + reset every series into dense int32 bucket counts and
+88-byte HistogramSummary records (snapshotHistograms,
+AdminMetricsExportTelemeter.scala:154-162).  Steps rotate over --rotate batches
+drawn with different seeds, so the engine's split/direct-tile choice (made from
+the previous batch) is tested on a batch it has not seen.
 
-Default workload (N=1): BASELINE config C3 on one GPU -- 1,000,000 series,
-1e9 samples, Zipf(s=1) series ids, log-normal values (synthetic; BASELINE.md
-§C3).  With --gpus N (torchrun, one rank per GPU) every rank owns its own
-1M-series shard (series-sharded, no collective on the data path): weak scaling.
---workload c4 (BASELINE config C4, fleet merge): the same 1M series are
-sample-sharded over the ranks (1e9 samples per step in total); each rank ingests
-its shard, exports dense state, the ranks reduce-scatter it over RCCL and each
-summarizes its series slice (strong scaling; collective time and bus GB/s are
-reported under "merge").
+Workloads (synthetic inputs generated on the GPU):
+  c3 (default)  1M series, 1e9 samples per step in total, Zipf(s=1) series ids,
+                log-normal values.  With N ranks the series space is split into
+                contiguous ranges of equal expected device time (a per-sample +
+                per-series cost model over the Zipf pmf, fleet.shard_ranges) and
+                each rank ingests the samples of its range: series-sharded, no
+                collective, strong scaling.
+  c4            fleet merge: the same 1M series, the 1e9 samples sample-sharded
+                over the ranks; each rank ingests its share and calls l5dh_merge
+                (export + RCCL reduce-scatter + summaries of its slice).
+  c2            100k series x 1k samples on one GPU (replicas when N > 1).
+  c1            1 series x 1e7 samples (replicas when N > 1).
+--piece P streams the batch from pinned host memory in P-sample l5dh_ingest
+calls (the JNI staging shape; PCIe-inclusive), instead of HBM-resident batches.
 
-Prints ONE JSON line (rank 0).  `value` = samples/s over all ranks;
-`roofline` = the dominant kernel's algorithmic bytes / its average duration
-(HIP events on the engine's stream); `path_roofline` = BASELINE's B_alg
-(8 B/sample + 7280 B/series) / ms_per_step; `cpu_baseline` = the C oracle
-(restatement of the JVM path, per-series mutex) on host cores.
+Launch: `python bench.py --gpus N` spawns N ranks itself (torch.distributed.run,
+before any GPU call); under torchrun (WORLD_SIZE set) it is one rank.  Rank 0
+prints ONE JSON line: `value` = samples/s over all ranks (max-over-ranks time);
+`roofline` = the dominant kernel's algorithmic bytes / its
+average duration (HIP events on the engine's stream); `path_roofline` = B_alg
+(8 B/sample + 7280 B/series) / ms_per_step -- the headline fraction;
+`cpu_baseline` = the C oracle (restatement of the JVM path) on host cores.
 """
 from __future__ import annotations
 
@@ -28,6 +37,10 @@ import argparse
 import ctypes
 import json
 import os
+import platform
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,14 +48,20 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+S_C3, N_C3 = 1_000_000, 1_000_000_000
+# algorithmic bytes per launch: 8 B per sample read once, 7192 B of
+# final counts + 88 B of summary written once per series; partition / sort passes,
+# zeroing and re-reads of records are not credited
 KERNEL_ALG_BYTES = {
-    # algorithmic bytes per launch, per unit
-    "count": lambda n, s: 4 * n,                  # reads series ids
-    "bin1": lambda n, s: 8 * n + 4 * n,           # reads (series, value), writes 4-B level-1 record
-    # bin2 moves only the records of non-direct tiles (a data-dependent share of n):
-    # it is timed but not priced
-    "accum": lambda n, s: 4 * n + 7280 * s,       # reads final record, writes counts + summary
+    "bin1": lambda n, s, fleet: 8 * n,                         # reads (series, value) once
+    "accum": lambda n, s, fleet: (7192 if fleet else 7280) * s,  # writes counts (+ summary)
 }
+METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
+# device cost model of one step on MI355X, for the C3 shard plan (round-2 kernel
+# times: C3 ingest 5.25 ms / 1e9 samples + accumulate ~1.3 ps per record; a 241K-
+# series shard accumulates in 0.41 ms; profiles/r02_*_bench.json)
+COST_PS_PER_SAMPLE = 6.5
+COST_PS_PER_SERIES = 1700.0
 
 
 def parse():
@@ -51,89 +70,151 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=["c3", "c2", "c1", "c4"], default="c3")
-    p.add_argument("--series", type=int, default=None, help="series per rank (default: workload's)")
-    p.add_argument("--samples", type=int, default=None, help="samples per rank per step (default: workload's)")
+    p.add_argument("--rotate", type=int, default=3, help="distinct batches (seeds) cycled over the steps")
+    p.add_argument("--piece", type=int, default=0, help="stream from pinned host memory in calls of this many samples")
+    p.add_argument("--shard", default=None, help="r/W: run rank r's C3 shard of a W-way split on this one GPU")
+    p.add_argument("--series", type=int, default=None, help="series (default: workload's)")
+    p.add_argument("--samples", type=int, default=None, help="samples per step in total (default: workload's)")
     p.add_argument("--bin-mode", type=int, default=0)
-    p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..512)")
+    p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..255)")
     p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
     p.add_argument("--split-min", type=int, default=None, help="engine param: min records of a split tile")
-    p.add_argument("--cpu-sample", type=int, default=20_000_000, help="samples in the CPU baseline sample (0: skip)")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-sample", type=int, default=None, help="samples in the CPU baseline sample (0: skip)")
+    p.add_argument("--cpu-threads", type=int, default=None, help="oracle threads (default: c1 1, else the host's)")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_latest.json"))
+    p.add_argument("--dry-run", action="store_true", help="ranks + shard plan only (gloo, no GPU, no engine)")
     return p.parse_args()
 
 
-def workload_defaults(args):
-    if args.workload == "c3":
-        S, N = 1_000_000, 1_000_000_000
-    elif args.workload == "c4":  # N = this rank's share of the 1e9 samples
-        S, N = 1_000_000, 1_000_000_000 // int(os.environ.get("WORLD_SIZE", "1"))
-    elif args.workload == "c2":
-        S, N = 100_000, 100_000_000
+# ---------------------------------------------------------------- launch
+def spawn(args) -> int:
+    """--gpus N without torchrun: start N ranks as children of this process (which
+    never touches the GPU) and exit with their status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------- workload plan
+def plan(args, world: int, rank: int) -> dict:
+    """What this rank ingests per step: series range / count, samples, generator
+    parameters.  Pure host arithmetic (no GPU)."""
+    import numpy as np
+    from linkerd_amd import fleet, synth
+    wl = args.workload
+    if args.shard:
+        rank, world = (int(x) for x in args.shard.split("/"))
+    if wl in ("c3", "c4"):
+        S = args.series or S_C3
+        N = args.samples or N_C3
+        cdf = synth.zipf_cdf(S)
+        if wl == "c4":  # sample-sharded: every rank the whole series space
+            n = N // world + (1 if rank < N % world else 0)
+            base = rank * (N // world) + min(rank, N % world)
+            return dict(workload=wl, S_total=S, N_total=N, first=0, count=S, samples=n, base_index=base,
+                        world=world, rank=rank, scaling="strong")
+        # balanced by expected device time: COST_PS_PER_SAMPLE per Zipf-expected
+        # sample + COST_PS_PER_SERIES per series row (balancing by samples alone
+        # would leave the last rank most of the dense series rows)
+        pmf = np.diff(np.concatenate([[0.0], cdf]))
+        shards = fleet.shard_ranges(S, world, weights=COST_PS_PER_SAMPLE * N * pmf + COST_PS_PER_SERIES)
+        sh = shards[rank]
+        mass = [float(cdf[x.first + x.count - 1] - (cdf[x.first - 1] if x.first else 0.0)) if x.count else 0.0
+                for x in shards]
+        ns = [int(round(N * m)) for m in mass]
+        ns[-1] = N - sum(ns[:-1])
+        base = sum(ns[:rank])
+        return dict(workload=wl, S_total=S, N_total=N, first=sh.first, count=sh.count, samples=ns[rank],
+                    base_index=base, world=world, rank=rank, scaling="strong",
+                    shard_samples=ns, shard_series=[x.count for x in shards])
+    if wl == "c2":
+        S, N = args.series or 100_000, args.samples or 100_000_000
     else:
-        S, N = 1, 10_000_000
-    return args.series or S, args.samples or N
+        S, N = args.series or 1, args.samples or 10_000_000
+    return dict(workload=wl, S_total=S * world, N_total=N * world, first=rank * S, count=S, samples=N,
+                base_index=0, world=world, rank=rank, scaling="weak")
 
 
-def gen_inputs(torch, synth_lib, workload, S, N, rank, stream):
+def gen_batch(torch, synth_lib, pl, seed_off, stream):
+    """One batch of this rank's samples in HBM (l5dh_synth.hip, the synth.py recipe)."""
+    import numpy as np
+    from linkerd_amd import synth
     dev = torch.device("cuda", torch.cuda.current_device())
-    series = torch.empty(N, dtype=torch.int32, device=dev)
-    values = torch.empty(N, dtype=torch.float32, device=dev)
-    sp = ctypes.c_void_p(series.data_ptr())
-    vp = ctypes.c_void_p(values.data_ptr())
-    if workload in ("c3", "c4"):
-        from linkerd_amd import synth
-        cdf = torch.from_numpy(synth.zipf_cdf(S)).to(dev)
-        # c3: every rank its own series shard; c4: one series space, rank r draws samples [r N, (r+1) N)
-        rc = synth_lib.l5ds_gen_zipf(sp, vp, ctypes.c_uint64(N), ctypes.c_uint64(S), ctypes.c_void_p(cdf.data_ptr()),
-                                     ctypes.c_uint64(3), ctypes.c_double(0.8), ctypes.c_uint64(rank * N),
-                                     ctypes.c_uint32(rank * S if workload == "c3" else 0), ctypes.c_void_p(stream))
-    elif workload == "c2":
-        K = N // S
-        rc = synth_lib.l5ds_gen_c2(sp, vp, ctypes.c_uint64(S), ctypes.c_uint64(K), ctypes.c_uint64(2),
-                                   ctypes.c_double(0.8), ctypes.c_uint32(rank * S), ctypes.c_void_p(stream))
+    n = pl["samples"]
+    series = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    values = torch.empty(max(n, 1), dtype=torch.float32, device=dev)[:n]
+    sp, vp = ctypes.c_void_p(series.data_ptr()), ctypes.c_void_p(values.data_ptr())
+    wl = pl["workload"]
+    if wl in ("c3", "c4"):
+        cdf = synth.zipf_cdf(pl["S_total"])
+        f, c = pl["first"], pl["count"]
+        lo = cdf[f - 1] if f else 0.0
+        sub = (cdf[f:f + c] - lo) / (cdf[f + c - 1] - lo)  # Zipf restricted to this rank's range
+        sub[-1] = 1.0
+        dcdf = torch.from_numpy(np.ascontiguousarray(sub)).to(dev)
+        rc = synth_lib.l5ds_gen_zipf(sp, vp, ctypes.c_uint64(n), ctypes.c_uint64(c), ctypes.c_void_p(dcdf.data_ptr()),
+                                     ctypes.c_uint64(3 + seed_off), ctypes.c_double(0.8),
+                                     ctypes.c_uint64(pl["base_index"]), ctypes.c_uint32(f), ctypes.c_void_p(stream))
+    elif wl == "c2":
+        S = pl["count"]
+        rc = synth_lib.l5ds_gen_c2(sp, vp, ctypes.c_uint64(S), ctypes.c_uint64(n // S), ctypes.c_uint64(2 + 16 * seed_off),
+                                   ctypes.c_double(0.8), ctypes.c_uint32(pl["first"]), ctypes.c_void_p(stream))
     else:
-        rc = synth_lib.l5ds_gen_c1(vp, sp, ctypes.c_uint64(N), ctypes.c_uint64(1 + rank), ctypes.c_void_p(stream))
+        rc = synth_lib.l5ds_gen_c1(vp, sp, ctypes.c_uint64(n), ctypes.c_uint64(1 + pl["rank"] + 16 * seed_off),
+                                   ctypes.c_void_p(stream))
     assert rc == 0, "synthetic generator launch failed"
     torch.cuda.synchronize()
     return series, values
 
 
-# engine timer -> the kernels it brackets (names as in tools/pmc_summary.py)
-# (steady state: the accumulate timer brackets the persistent cold kernel and the split kernel)
-PMC_PARTS = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold_p", "accum_split"]}
-
-
-def load_pmc_traffic(path, workload, S, N):
-    """HBM bytes per launch from a committed PMC summary (tools/profile_pmc.sh +
-    tools/pmc_summary.py) of the same workload; {} if absent or for another one."""
+# ---------------------------------------------------------------- baselines / profiles
+def host_cpu():
+    model = platform.processor() or ""
     try:
-        pm = json.load(open(path))
-    except (OSError, ValueError):
-        return {}
-    if pm.get("workload") != workload or pm.get("series") != S or pm.get("samples") != N:
-        return {}
-    ks = pm.get("kernels", {})
-    out = {}
-    for name, parts in PMC_PARTS.items():
-        if all(p in ks and "hbm_bytes_per_launch" in ks[p] for p in parts):
-            out[name] = int(sum(ks[p]["hbm_bytes_per_launch"] for p in parts))
-    return out
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the GPU box's CPU share per GPU
+    return model, nproc, avail, (min(avail, share) if share > 0 else avail)
 
 
-def cpu_baseline(workload, S, N, sample, threads):
-    """C oracle (restatement of the JVM Metric.Stat path) on a bounded sample:
-    ingest `sample` samples of the same recipe with `threads` workers (per-series
-    mutex, Metric.scala:30) and snapshot all S series on one thread (the timer
-    thread, AdminMetricsExportTelemeter.scala:154-162); extrapolate to one full
-    step (N samples + S summaries)."""
-    import numpy as np
+def java_probe() -> str:
+    j = shutil.which("java")
+    if not j:
+        return "absent (no `java` on PATH): the JVM reference path cannot run; the C restatement is timed instead"
+    try:
+        r = subprocess.run([j, "-version"], capture_output=True, text=True, timeout=20)
+        return (r.stderr or r.stdout).strip().splitlines()[0]
+    except Exception as e:  # noqa: BLE001
+        return f"java present but -version failed: {e}"
+
+
+def cpu_baseline(pl, sample, threads):
+    """C oracle (restatement of the JVM Metric.Stat path: per-series mutex, binary
+    search, int32[1798] per series, 8-scan summary) on a bounded sample of the same
+    recipe: `sample` samples ingested with `threads` workers, then all series
+    snapshot on ONE thread (the timer thread, AdminMetricsExportTelemeter.scala:154-162),
+    extrapolated to one full step."""
     from linkerd_amd import synth
     from oracle import oracle as O
+    wl, S, N = pl["workload"], pl["count"], pl["samples"]
     n = min(sample, N)
-    if workload in ("c3", "c4"):
+    if wl in ("c3", "c4"):
         s, v = synth.c3(S=S, N=n)
-    elif workload == "c2":
+    elif wl == "c2":
         s, v = synth.c2(S=S, K=max(1, n // S))
         n = s.size
     else:
@@ -142,29 +223,62 @@ def cpu_baseline(workload, S, N, sample, threads):
     h.ingest(s[: min(n, 100_000)], v[: min(n, 100_000)], threads=threads)  # first-touch warmup
     h = O.OracleHistograms(S)
     t0 = time.perf_counter()
-    rc = h.ingest(s, v, threads=threads)
+    assert h.ingest(s, v, threads=threads) == 0
     t_ing = time.perf_counter() - t0
-    assert rc == 0
     t0 = time.perf_counter()
     h.snapshot(reset=True)
     t_snap = time.perf_counter() - t0
     full = t_ing * (N / n) + t_snap
+    model, nproc, avail, _ = host_cpu()
     return {"value": N / full, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{workload} recipe, {n} samples ingested with {threads} threads ({t_ing:.2f} s) + snapshot "
-                      f"of all {S} series on 1 thread ({t_snap:.2f} s), extrapolated to {N} samples/step; "
-                      "C restatement of the JVM path (no JDK/finagle jar on the box), per-series mutex"}
+            "sample": f"{wl} recipe, {n} samples ingested with {threads} thread(s) ({t_ing:.2f} s) + snapshot of all "
+                      f"{S} series on 1 thread ({t_snap:.2f} s), extrapolated to {N} samples/step",
+            "cpu_model": model, "nproc": nproc, "cpus_available": avail, "java": java_probe(),
+            "note": "C restatement of the JVM path (oracle/hist_oracle.c); no JDK/finagle-stats jar on the box"}
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+def load_pmc_traffic(path, pl):
+    """HBM bytes per launch from a committed PMC summary (tools/profile_pmc.sh +
+    tools/pmc_summary.py) of the same workload and the same engine sources."""
+    from linkerd_amd._native import engine_source_hash
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return {}, "no PMC summary"
+    if pm.get("workload") != pl["workload"] or pm.get("series") != pl["count"] or pm.get("samples") != pl["samples"]:
+        return {}, "PMC summary is of another workload"
+    if pm.get("src_hash") != engine_source_hash():
+        return {}, "stale: PMC summary measured other engine sources (re-run tools/profile_pmc.sh)"
+    parts = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold_p", "accum_split"]}
+    ks = pm.get("kernels", {})
+    out = {name: int(sum(ks[p]["hbm_bytes_per_launch"] for p in ps)) for name, ps in parts.items()
+           if all(p in ks and "hbm_bytes_per_launch" in ks[p] for p in ps)}
+    return out, f"PMC {os.path.basename(path)} (src {pm['src_hash']})"
 
+
+# ---------------------------------------------------------------- main
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    import torch
+    import torch.distributed as dist
+
+    pl = plan(args, world, rank)
+    if args.dry_run:  # the rank harness without a device (CPU tests)
+        if distributed:
+            dist.init_process_group("gloo")
+            plans = [None] * world
+            dist.all_gather_object(plans, pl)
+        else:
+            plans = [pl]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "world": world, "plans": plans}), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return
+
     if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -179,43 +293,62 @@ def main():
     for fn in ("l5ds_gen_c1", "l5ds_gen_c2", "l5ds_gen_zipf"):
         getattr(synth_lib, fn).restype = ctypes.c_int
 
-    S, N = workload_defaults(args)
     stream = torch.cuda.current_stream().cuda_stream
-    series, values = gen_inputs(torch, synth_lib, args.workload, S, N, rank, stream)
+    fleet = pl["workload"] == "c4"
+    streaming = args.piece > 0
+    R = 1 if streaming else max(1, args.rotate)
+    batches = [gen_batch(torch, synth_lib, pl, k, stream) for k in range(R)]
+    S = pl["count"]
+    n = pl["samples"]
 
     eng = HistogramEngine(S, device=torch.cuda.current_device())
     eng.set_param(N_.PARAM_BIN_MODE, args.bin_mode)
-    if args.direct_max is not None:
-        eng.set_param(N_.PARAM_DIRECT_MAX, args.direct_max)
-    if args.direct_div is not None:
-        eng.set_param(N_.PARAM_DIRECT_DIV, args.direct_div)
-    if args.split_min is not None:
-        eng.set_param(N_.PARAM_SPLIT_MIN, args.split_min)
-    fleet = args.workload == "c4"
-    summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
-    counts = torch.empty((S, N_.NBUCKETS), dtype=torch.int32, device=dev)
-    totals = torch.empty(S, dtype=torch.int64, device=dev)
-    merged = {}
-    merge_ev = []
+    for prm, v in ((N_.PARAM_DIRECT_MAX, args.direct_max), (N_.PARAM_DIRECT_DIV, args.direct_div),
+                   (N_.PARAM_SPLIT_MIN, args.split_min)):
+        if v is not None:
+            eng.set_param(prm, v)
+    if fleet:
+        if distributed:
+            obj = [HistogramEngine.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            eng.comm_init_rank(obj[0], world, rank)
+        else:
+            eng.comm_init_rank(HistogramEngine.comm_unique_id(), 1, 0)
+    rows = eng.merge_rows() if fleet else S
+    summ = torch.empty((max(rows, 1), 11), dtype=torch.int64, device=dev)
+    counts = None if fleet else torch.empty((max(S, 1), N_.NBUCKETS), dtype=torch.int32, device=dev)
+
+    host = None
+    if streaming:  # the batch in pinned host memory (l5dh_pin_alloc, what the JNI side stages into)
+        lib = N_.load()
+        hs, hv = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.l5dh_pin_alloc(max(n, 1) * 4, ctypes.byref(hs)) == 0
+        assert lib.l5dh_pin_alloc(max(n, 1) * 4, ctypes.byref(hv)) == 0
+        for dst, src in zip((hs, hv), batches[0]):
+            h = src.cpu().numpy()  # keep the host copy alive across the memmove
+            ctypes.memmove(dst, h.ctypes.data, n * 4)
+            del h
+        host = (lib, hs.value, hv.value)
+        batches = [None]
+
+    state = {"k": 0, "merged": None}
 
     def step():
-        eng.ingest(series, values)
-        if not fleet:
-            eng.snapshot_into(summ, counts, reset=True)
-            return
-        # C4: dense partial state -> reduce-scatter (RCCL) -> summaries of this rank's slice
-        eng.export_state(counts=counts, totals=totals, reset=True)
-        if merge_ev:
-            merge_ev[0].record()
-        if distributed:
-            from linkerd_amd.fleet import fleet_merge
-            c, t, first = fleet_merge(counts, totals, mode="reduce_scatter")
+        b = batches[state["k"] % R]
+        state["k"] += 1
+        if host:
+            lib, hs, hv = host
+            for off in range(0, n, args.piece):
+                m = min(args.piece, n - off)
+                rc = lib.l5dh_ingest(eng._ctx, hs + 4 * off, hv + 4 * off, m)
+                if rc:
+                    eng._check(rc, "l5dh_ingest")
         else:
-            c, t, first = counts, totals, 0
-        if merge_ev:
-            merge_ev[1].record()
-        eng.summarize_dense(c, t, out=summ[:c.shape[0]])
-        merged.update(c=c, n=c.shape[0])
+            eng.ingest(*b)
+        if fleet:
+            state["merged"] = eng.merge(N_.MERGE_REDUCE_SCATTER, out=summ)
+        else:
+            eng.snapshot_into(summ, counts, reset=True)
 
     def barrier():
         if distributed:
@@ -238,33 +371,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # sanity: every sample landed in exactly one bucket of the last snapshot
+    # sanity: every sample of the last step landed in exactly one bucket
     if fleet:
-        tot = torch.stack([merged["c"].sum(dtype=torch.int64), summ[:merged["n"], 0].sum()])
-        if distributed:
-            dist.all_reduce(tot)
-        want = N * world
+        first, cnt = state["merged"]
+        tot = torch.stack([summ[:cnt, 0].sum(), torch.tensor(0, device=dev)])
+        want = pl["N_total"]
     else:
-        tot = torch.stack([counts.sum(dtype=torch.int64), summ[:, 0].sum()])
-        want = N
-    if not os.environ.get("L5DH_DBG"):  # L5DH_DBG selects timing-only kernel variants
-        assert int(tot[0].item()) == want, f"bucket counts sum {int(tot[0].item())} != {want}"
+        tot = torch.stack([counts[:S].sum(dtype=torch.int64), summ[:S, 0].sum()])
+        want = n
+    if distributed and fleet:
+        dist.all_reduce(tot)
+    assert int(tot[0].item()) == want, f"summary counts sum {int(tot[0].item())} != {want}"
+    if not fleet:
         assert int(tot[1].item()) == want
-
-    merge = None
-    if fleet:  # collective time alone (events around the reduce-scatter, separate steps)
-        merge_ev[:] = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-        ms = []
-        for _ in range(3):
-            step()
-            torch.cuda.synchronize()
-            ms.append(merge_ev[0].elapsed_time(merge_ev[1]))
-        merge_ev.clear()
-        cms = sorted(ms)[1]
-        nbytes = S * (N_.NBUCKETS * 4 + 8)  # int32 counts + int64 total per series, per rank
-        merge = {"collective": "reduce_scatter (RCCL)" if distributed else "none (1 rank)",
-                 "collective_ms": round(cms, 4), "bytes_per_rank": nbytes,
-                 "bus_GBs": round(nbytes * (world - 1) / world / (cms * 1e-3) / 1e9, 1) if world > 1 else None}
 
     # per-kernel device time (HIP events on the engine's stream), separate steps
     eng.set_param(N_.PARAM_TIMING, 1)
@@ -274,11 +393,11 @@ def main():
         step()
     kt = eng.kernel_times(reset=True)
     eng.set_param(N_.PARAM_TIMING, 0)
+    barrier()
 
     ms_per_step = elapsed / args.steps * 1e3
-    total_samples = N * world
+    total_samples = pl["N_total"] if pl["scaling"] == "strong" and not args.shard else n * world
     value = total_samples * args.steps / elapsed
-    balg = 8 * N + 7280 * S if not fleet else 8 * N + 7280 * S // world  # c4: a rank writes its slice
     kernels = {}
     for name, (ms, launches) in kt.items():
         if launches == 0:
@@ -286,50 +405,86 @@ def main():
         avg = ms / launches
         entry = {"avg_ms": round(avg, 4), "launches_per_step": round(launches / tsteps, 2)}
         if name in KERNEL_ALG_BYTES:
-            ab = KERNEL_ALG_BYTES[name](N, S) / (launches / tsteps)
+            ab = KERNEL_ALG_BYTES[name](n, S, fleet) / (launches / tsteps)
             entry["alg_GBs"] = round(ab / (avg * 1e-3) / 1e9, 1)
             entry["alg_bytes"] = int(ab)
         kernels[name] = entry
-    dom = max((k for k in kernels if k in KERNEL_ALG_BYTES), key=lambda k: kernels[k]["avg_ms"])
-    d = kernels[dom]
-    pmc = load_pmc_traffic(args.pmc_json, args.workload, S, N)
+    pmc, pmc_note = load_pmc_traffic(args.pmc_json, pl)
     for name, entry in kernels.items():
         if name in pmc:
             entry["traffic"] = pmc[name]
-    traffic = pmc.get(dom)
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": d["alg_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(d["alg_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": d["alg_bytes"], "avg_launch_ms": d["avg_ms"]}
+    priced = [k for k in kernels if k in KERNEL_ALG_BYTES]
+    roofline = None
+    if priced:
+        dom = max(priced, key=lambda k: kernels[k]["avg_ms"])
+        d = kernels[dom]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": d["alg_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(d["alg_GBs"] / HBM_PEAK_GBS, 4), "traffic": pmc.get(dom), "traffic_source": pmc_note,
+                    "alg_bytes_per_launch": d["alg_bytes"], "avg_launch_ms": d["avg_ms"],
+                    "pricing": "SURVEY.md §8d: bin1 8 B/sample, accum 7280 B/series (7192 for the c4 export)"}
+    # path: B_alg of everything this step processed, over the step time and all GPUs' peak
+    rows_summarized = pl["S_total"] if not args.shard else S
+    balg = 8 * (total_samples if not args.shard else n) + 7280 * rows_summarized
+    gpus = 1 if args.shard else world
     path_gbs = balg / (ms_per_step * 1e-3) / 1e9
+    merge = None
+    if fleet and "merge" in kt and kt["merge"][1]:
+        cms = kt["merge"][0] / kt["merge"][1]
+        nbytes = eng.merge_rows() * world * (N_.NBUCKETS * 4 + 8)
+        merge = {"collective": "RCCL reduce-scatter (l5dh_merge)" if world > 1 else "RCCL reduce-scatter, 1 rank",
+                 "collective_ms": round(cms, 4), "bytes_per_rank": nbytes,
+                 "bus_GBs": round(nbytes * (world - 1) / world / (cms * 1e-3) / 1e9, 1) if world > 1 else None}
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args.workload, S, N, args.cpu_sample, args.cpu_threads)
+    sample = args.cpu_sample if args.cpu_sample is not None else (10_000_000 if pl["workload"] == "c1" else 20_000_000)
+    if rank == 0 and world == 1 and sample > 0 and not streaming:
+        threads = args.cpu_threads or (1 if pl["workload"] == "c1" else host_cpu()[3])
+        cpu = cpu_baseline(pl, sample, threads)
     if rank == 0:
+        wl_names = {"c3": "C3: 1M series, 1e9 Zipf(s=1) samples per step, log-normal values",
+                    "c2": "C2: 100k series x 1k samples, permuted COO",
+                    "c1": "C1: 1 series x 1e7 log-normal samples",
+                    "c4": "C4: fleet merge, 1M series, 1e9 Zipf(s=1) samples per step sample-sharded over the "
+                          "ranks, RCCL reduce-scatter of dense counts, summaries of each rank's slice"}
+        cfg = {"workload": wl_names[pl["workload"]], "series_total": pl["S_total"], "samples_per_step": total_samples,
+               "series_per_gpu": S, "samples_per_gpu_per_step": n, "rotating_batches": R,
+               "parallelism": (f"sample-sharded x{world}" if fleet else
+                               f"series-sharded x{world} (weighted ranges)" if pl["workload"] == "c3" else
+                               f"replicas x{world}"),
+               "step": ("ingest + l5dh_merge (export, reduce-scatter, slice summaries)" if fleet else
+                        "ingest (count+scan+bin1+bin2) + snapshot(reset, dense counts + summaries)")}
+        if args.shard:
+            cfg["shard"] = f"rank {pl['rank']} of {pl['world']}: series [{pl['first']}, {pl['first'] + S}), {n} samples"
+        if streaming:
+            cfg["ingest"] = (f"pinned host memory (l5dh_pin_alloc), {args.piece}-sample l5dh_ingest calls: "
+                             "PCIe-inclusive, not the HBM-resident headline")
         line = {
-            "metric": "histogram samples ingested+summarized/sec (1M series) and % HBM peak",
-            "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong" if fleet else "weak", "vs_baseline": None,
-            "dtype": "u32", "data": "synthetic",
-            "config": {"workload": {"c3": "C3: 1M series x 1e9 samples, Zipf(s=1) ids, log-normal values",
-                                    "c2": "C2: 100k series x 1k samples, permuted COO",
-                                    "c1": "C1: 1 series x 1e7 log-normal samples",
-                                    "c4": "C4: fleet merge, 1M series, 1e9 Zipf(s=1) samples per step "
-                                          "sample-sharded over the ranks, reduce-scatter of dense counts"}[args.workload],
-                       "series_per_gpu": S, "samples_per_gpu_per_step": N, "parallelism": f"{'sample-sharded' if fleet else 'series-sharded'} x{world}",
-                       "step": "ingest (count+scan+bin1+bin2) + snapshot(reset, dense counts + summaries)"},
-            "roofline": roofline,
-            "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(path_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_step": balg,
-                              "formula": "8 B/sample + 7280 B/series (BASELINE.md)"},
-            "kernels": kernels,
-            "cpu_baseline": cpu,
+            "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": pl["scaling"], "vs_baseline": None, "dtype": "u32", "data": "synthetic", "config": cfg,
+            "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS * gpus,
+                              "unit": "GB/s", "frac": round(path_gbs / (HBM_PEAK_GBS * gpus), 4),
+                              "alg_bytes_per_step": balg, "formula": "8 B/sample + 7280 B/series (SURVEY.md §8d)"},
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
         if merge:
             line["merge"] = merge
         print(json.dumps(line), flush=True)
+    if host:
+        host[0].l5dh_pin_free(ctypes.c_void_p(host[1]))
+        host[0].l5dh_pin_free(ctypes.c_void_p(host[2]))
     eng.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if os.environ.get("L5DH_DBG"):
+        sys.exit("bench.py: L5DH_DBG is set -- it selects timing-only kernel variants (results invalid) in "
+                 "development builds; unset it for a bench line")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args))
+    run(args)
 
 
 if __name__ == "__main__":

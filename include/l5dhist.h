@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define L5DH_ABI_VERSION 1
+#define L5DH_ABI_VERSION 2 /* 2: staging ring, deferred id errors, RCCL merge, NULL = null stream */
 #define L5DH_NLIMITS 1797  /* BucketedHistogram.scala:42 (0.5% error => 1797 limits) */
 #define L5DH_NBUCKETS 1798 /* counts = limits.length + 1 (upstream finagle-stats) */
 #define L5DH_MAX_SERIES (1u << 20) /* per context (= per GPU); shard wider fleets */
@@ -70,8 +70,18 @@ enum {
   L5DH_PARAM_BIN_MODE = 5,     /* 0 auto, 1 single-level scatter, 2 two-level partition */
   L5DH_PARAM_DIRECT_MAX = 6,   /* tiles whose final records k_bin1 writes directly (0..255) */
   L5DH_PARAM_DIRECT_DIV = 7,   /* direct tiles average >= 1/div records per 8K-sample sub-chunk */
-  L5DH_PARAM_SPLIT_MIN = 8     /* tiles laid out per half-tile have >= this many records per batch */
+  L5DH_PARAM_SPLIT_MIN = 8,    /* tiles laid out per half-tile have >= this many records per batch */
+  L5DH_PARAM_STAGE_SAMPLES = 9, /* device staging ring for small batches, in samples (0: off) */
+  L5DH_PARAM_MAX_SLABS = 10,   /* ingest slabs (workgroups of the partition kernels), 1..512 */
+  L5DH_PARAM_MERGE_RCCL_1RANK = 11 /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
 };
+
+/* Fleet-merge modes for l5dh_merge */
+enum {
+  L5DH_MERGE_REDUCE_SCATTER = 0, /* rank r receives the summed rows of its series slice */
+  L5DH_MERGE_ALL_REDUCE = 1      /* every rank receives all summed rows */
+};
+#define L5DH_UNIQUE_ID_BYTES 128 /* = NCCL_UNIQUE_ID_BYTES */
 
 /* Kernel ids for l5dh_kernel_time */
 enum {
@@ -82,7 +92,8 @@ enum {
   L5DH_K_HOT = 4,    /* split-tile init/finish and row summaries */
   L5DH_K_COPY = 5,   /* H2D/D2H staging copies */
   L5DH_K_BIN2 = 6,   /* level-2 partition (super-tile runs -> per-tile segments) */
-  L5DH_K_NKERNELS = 7
+  L5DH_K_MERGE = 7,  /* the RCCL collective of l5dh_merge */
+  L5DH_K_NKERNELS = 8
 };
 
 /* Reference: BucketedHistogram() per Stat (MetricsTree.scala:88).  Opens a
@@ -97,9 +108,20 @@ const int32_t* l5dh_limits(size_t* n);
 
 /* Reference: Metric.Stat.add(Float) (Metric.scala:30-33), batched: adds
  * values[i] to series series[i] for i < n.  Integer-only effect, so order
- * independent.  Samples with out-of-range ids are dropped and the call
- * returns -EINVAL after ingesting the valid ones.  Returns once the batch is
- * binned on the device (no caller pointer is retained). */
+ * independent.
+ *
+ * Small batches (n <= half the staging ring, L5DH_PARAM_STAGE_SAMPLES) are
+ * appended to a device staging ring and binned together when it fills or at
+ * the next snapshot / peek / export / merge / sync; larger batches are binned
+ * at once.  The call does not wait for the binning kernels: host buffers may
+ * be reused as soon as it returns (their copy has completed); device buffers
+ * may be reused once it returns when the context runs on its own stream, and
+ * in stream order when it runs on a caller stream (l5dh_set_stream).
+ *
+ * Samples with out-of-range ids are dropped.  The kernels detect them
+ * asynchronously: the error is reported as -EINVAL by a later l5dh_ingest
+ * (once the device has flagged it) or at the latest by l5dh_sync, once per
+ * occurrence; all valid samples are ingested. */
 int l5dh_ingest(l5dh_ctx* ctx, const uint32_t* series, const float* values, size_t n);
 
 /* Reference: Metric.Stat.snapshot() + reset() per Stat as driven by
@@ -127,11 +149,50 @@ int l5dh_export_state(l5dh_ctx* ctx, uint32_t first, uint32_t count, int32_t* co
 int l5dh_summarize_dense(l5dh_ctx* ctx, const int32_t* counts, const int64_t* totals, size_t n,
                          l5dh_summary* out);
 
-/* Wait for queued work; returns a deferred ingest error if any. */
+/* Fleet merge over RCCL (xGMI): sample-sharded series (config C4) summed across
+ * contexts on different GPUs.  One communicator per context, one rank per GPU:
+ *  - multi-process (or one thread per context): rank 0 calls l5dh_comm_unique_id,
+ *    the caller distributes the L5DH_UNIQUE_ID_BYTES bytes, every rank calls
+ *    l5dh_comm_init_rank (collective: all ranks must call it);
+ *  - one process holding several GPUs (e.g. a JVM): l5dh_comm_init_all over its
+ *    contexts (distinct devices; rank i = ctxs[i]).
+ * Every context of a communicator has the same max_series. */
+int l5dh_comm_unique_id(void* id_out /* L5DH_UNIQUE_ID_BYTES */);
+int l5dh_comm_init_rank(l5dh_ctx* ctx, const void* id, int nranks, int rank);
+int l5dh_comm_init_all(l5dh_ctx** ctxs, int n);
+int l5dh_comm_destroy(l5dh_ctx* ctx);
+
+/* Reference: the snapshot of a series whose samples arrived on several hosts
+ * must see their merged counts (AdminMetricsExportTelemeter.scala:154-162,
+ * Metric.scala:39-67).  Collective (every rank of the communicator calls it):
+ * each rank's pending samples and state are exported (whole range, reset), the
+ * int32 counts [S][1798] and int64 totals [S] are summed with one RCCL
+ * reduce-scatter (or all-reduce), and the rank summarizes the rows it received:
+ * series [*first, *first + *count) (reduce-scatter: slice r of ceil(S/nranks)
+ * rows; all-reduce: all S).  out (nullable) receives *count l5dh_summary,
+ * counts_out / totals_out (nullable) the summed rows.  Each output must hold
+ * ceil(S/nranks) rows (reduce-scatter) or S rows (all-reduce).  Integer sums:
+ * bit-exact and independent of the reduction order. */
+int l5dh_merge(l5dh_ctx* ctx, int mode, l5dh_summary* out, int32_t* counts_out, int64_t* totals_out,
+               uint32_t* first, uint32_t* count);
+/* The same for all contexts of an l5dh_comm_init_all communicator, from one
+ * thread (the collectives are grouped).  Arrays are indexed like ctxs; any of
+ * the output arrays (or their entries) may be NULL. */
+int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_t** counts_outs,
+                   int64_t** totals_outs, uint32_t* firsts, uint32_t* counts);
+
+/* Bin staged samples, wait for queued work; returns a deferred ingest error if any. */
 int l5dh_sync(l5dh_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the
- * context's own stream. */
+/* Run the context's work on an external hipStream_t, e.g. the caller's current
+ * stream (torch's), so the context's kernels are ordered with the caller's work
+ * on it; NULL selects the device's legacy default (null) stream.
+ * L5DH_OWN_STREAM restores the context's own stream (the default). */
+#define L5DH_OWN_STREAM ((void*)(intptr_t)-1)
 int l5dh_set_stream(l5dh_ctx* ctx, void* hip_stream);
+/* Order the context's next work after a caller's hipEvent_t (recorded on whatever
+ * stream produced the device inputs, e.g. a torch.cuda.Event): the context's
+ * stream waits for it on the device, the host does not. */
+int l5dh_wait_event(l5dh_ctx* ctx, void* hip_event);
 int l5dh_set_param(l5dh_ctx* ctx, int param, int64_t value);
 /* Accumulated device time (ms) and launch count of one kernel id since the
  * last reset (requires L5DH_PARAM_TIMING=1). reset_after != 0 zeroes it. */

@@ -34,9 +34,17 @@ PARAM_BIN_MODE = 5
 PARAM_DIRECT_MAX = 6
 PARAM_DIRECT_DIV = 7
 PARAM_SPLIT_MIN = 8
+PARAM_STAGE_SAMPLES = 9
+PARAM_MAX_SLABS = 10
+PARAM_MERGE_RCCL_1RANK = 11
 
-K_COUNT, K_SCAN, K_BIN, K_ACCUM, K_HOT, K_COPY, K_BIN2 = range(7)
-KERNEL_NAMES = ("count", "scan", "bin1", "accum", "hot", "copy", "bin2")
+MERGE_REDUCE_SCATTER = 0
+MERGE_ALL_REDUCE = 1
+UNIQUE_ID_BYTES = 128
+OWN_STREAM = ctypes.c_void_p(-1 & (2 ** 64 - 1)).value  # L5DH_OWN_STREAM
+
+K_COUNT, K_SCAN, K_BIN, K_ACCUM, K_HOT, K_COPY, K_BIN2, K_MERGE = range(8)
+KERNEL_NAMES = ("count", "scan", "bin1", "accum", "hot", "copy", "bin2", "merge")
 
 
 class NativeLibraryMissing(ImportError):
@@ -67,6 +75,7 @@ SIGNATURES = {
     "l5dh_summarize_dense": (_c.c_int, [_vp, _vp, _vp, _c.c_size_t, _vp]),
     "l5dh_sync": (_c.c_int, [_vp]),
     "l5dh_set_stream": (_c.c_int, [_vp, _vp]),
+    "l5dh_wait_event": (_c.c_int, [_vp, _vp]),
     "l5dh_set_param": (_c.c_int, [_vp, _c.c_int, _c.c_int64]),
     "l5dh_kernel_time": (_c.c_int, [_vp, _c.c_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64), _c.c_int]),
     "l5dh_device": (_c.c_int, [_vp, _c.POINTER(_c.c_int)]),
@@ -74,7 +83,27 @@ SIGNATURES = {
     "l5dh_pin_alloc": (_c.c_int, [_c.c_size_t, _c.POINTER(_vp)]),
     "l5dh_pin_free": (_c.c_int, [_vp]),
     "l5dh_last_error": (_c.c_char_p, [_vp]),
+    "l5dh_comm_unique_id": (_c.c_int, [_vp]),
+    "l5dh_comm_init_rank": (_c.c_int, [_vp, _vp, _c.c_int, _c.c_int]),
+    "l5dh_comm_init_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int]),
+    "l5dh_comm_destroy": (_c.c_int, [_vp]),
+    "l5dh_merge": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
+    "l5dh_merge_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.POINTER(_vp), _c.POINTER(_vp),
+                                  _c.POINTER(_vp), _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
 }
+
+
+def engine_source_hash() -> str:
+    """sha256 (16 hex) of the engine's kernel and host sources: ties committed
+    profiles (PMC traffic) to the code they measured."""
+    import hashlib
+    h = hashlib.sha256()
+    d = os.path.join(PKG_DIR, "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp")) and "synth" not in f:
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def header_symbols(path: str = HEADER_PATH) -> list:

@@ -9,6 +9,7 @@
 // every pending segment into LDS-private tile histograms and emits summaries
 // in the same pass (the fused path) or folds into state first (range path).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -173,7 +174,7 @@ struct l5dh_ctx {
   uint8_t* d_dirty = nullptr;
   uint32_t* d_err = nullptr;
   // scratch
-  uint32_t* d_table = nullptr;  // [G_max][F + COLS]
+  uint32_t* d_table = nullptr;  // [512][F + COLS] (G_max <= 512 slabs)
   uint32_t* d_tile_tot = nullptr;  // [F + COLS] column totals (ingest), tile totals (snapshot plan)
   uint32_t* d_cold_tile = nullptr;
   DevBuf hot_item;    // big-tile chunk items (sized per snapshot)
@@ -205,6 +206,17 @@ struct l5dh_ctx {
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
   uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
+  // staging ring: small ingest batches are concatenated on the device and binned together
+  DevBuf ring_series, ring_values;
+  size_t ring_fill = 0;
+  size_t ring_cap = 0;  // samples (0: every batch is binned at once)
+  hipEvent_t ev_copy = nullptr;
+  uint32_t err_reported = 0;  // invalid-id reports already returned (h_header[4] is the device's count)
+  // fleet merge (RCCL)
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  DevBuf merge_counts, merge_totals, recv_counts, recv_totals;
+  bool rccl_1rank = false;  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
   uint32_t hot_chunk = 1u << 18;  // records per big-tile item (u32 LDS bins, one half-tile per workgroup)
@@ -399,16 +411,15 @@ int fold(l5dh_ctx* c) {
   return aggregate(c, 0, 0, none);
 }
 
-// The ingest error flag comes back through pinned memory with the stream's one
-// synchronization (h_header[4]; a pageable copy would add a second round trip).
+// Invalid series ids: k_count adds to the device counter d_err (never reset);
+// every binned batch is followed by an asynchronous copy of it into pinned
+// h_header[4].  The host value only grows, so comparing it with the number of
+// reports already returned needs no synchronization.
 int check_err(l5dh_ctx* c) {
-  HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-  int r = sync_stream(c);
-  if (r) return r;
-  const uint32_t e = c->h_header[4];
-  if (e) {
-    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, c->stream));
-    return fail(c, -EINVAL, "series id >= max_series in ingest batch (samples dropped)");
+  const uint32_t seen = __atomic_load_n(c->h_header + 4, __ATOMIC_ACQUIRE);
+  if (seen != c->err_reported) {
+    c->err_reported = seen;
+    return fail(c, -EINVAL, "series id >= max_series in an ingest batch (those samples were dropped)");
   }
   return 0;
 }
@@ -472,10 +483,6 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
                               c->stream));
       c->split_cur ^= 1;
     }
-    if (getenv("L5DH_PRINT_ADDRS"))  // development: buffer placement
-      fprintf(stderr, "l5dh addrs: in %p %p scratch1 %p recs %p table %p (recs-scratch1 = %lld)\n", (const void*)ds,
-              (const void*)dv, c->scratch1.p, sg.recs.p, (void*)c->d_table,
-              (long long)((char*)sg.recs.p - (char*)c->scratch1.p));
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
@@ -492,9 +499,56 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   sg.n = n;
   c->nseg++;
-  // No caller pointer is retained past return: wait for the batch to be binned
-  // (the same synchronization brings the error flag back).
-  return check_err(c);
+  // the invalid-id counter follows the batch to the host asynchronously (check_err)
+  HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
+// Bin the staging ring as one batch.
+int flush_ring(l5dh_ctx* c) {
+  if (!c->ring_fill) return 0;
+  const size_t n = c->ring_fill;
+  c->ring_fill = 0;
+  return do_ingest(c, static_cast<const uint32_t*>(c->ring_series.p), static_cast<const float*>(c->ring_values.p), n);
+}
+
+// Wait until the caller's buffers of this call have been read by the device.
+int wait_inputs(l5dh_ctx* c) {
+  HIPCHK(c, hipEventRecord(c->ev_copy, c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_copy));
+  return 0;
+}
+
+int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n) {
+  if (n == 0) return 0;
+  const bool dev = is_device_ptr(series) && is_device_ptr(values);
+  // caller-stream contexts are stream ordered for device inputs; otherwise the
+  // call returns once nothing of the caller's memory is still to be read
+  const bool wait = !dev || c->stream == c->own_stream;
+  if (c->ring_cap && n <= c->ring_cap / 2) {
+    int r;
+    if (c->ring_fill + n > c->ring_cap && (r = flush_ring(c))) return r;
+    if ((r = ensure(c, c->ring_series, c->ring_cap * 4 + 64)) || (r = ensure(c, c->ring_values, c->ring_cap * 4 + 64)))
+      return r;
+    {
+      KTimer kt(c, L5DH_K_COPY);
+      HIPCHK(c, hipMemcpyAsync(static_cast<uint32_t*>(c->ring_series.p) + c->ring_fill, series, n * 4, hipMemcpyDefault,
+                               c->stream));
+      HIPCHK(c, hipMemcpyAsync(static_cast<float*>(c->ring_values.p) + c->ring_fill, values, n * 4, hipMemcpyDefault,
+                               c->stream));
+    }
+    c->ring_fill += n;
+    return wait ? wait_inputs(c) : 0;
+  }
+  int r = flush_ring(c);
+  if (r) return r;
+  // batches are binned in pieces below 2^30 samples (k_bin1 tags direct-tile
+  // destinations in bit 31)
+  for (size_t o = 0; o < n; o += MAX_BATCH) {
+    const size_t m = std::min(n - o, MAX_BATCH);
+    if ((r = do_ingest(c, series + o, values + o, m))) return r;
+  }
+  return wait ? wait_inputs(c) : 0;
 }
 
 bool full_range(l5dh_ctx* c, uint32_t first, uint32_t count) { return first == 0 && count == c->S; }
@@ -502,7 +556,8 @@ bool full_range(l5dh_ctx* c, uint32_t first, uint32_t count) { return first == 0
 int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {
   if ((uint64_t)first + count > c->S) return fail(c, -EINVAL, "series range out of bounds");
   if (count == 0) return 0;
-  int r;
+  int r = flush_ring(c);
+  if (r) return r;
   // outputs: device pointers are written directly, host pointers via staging
   Summary88* d_summ = nullptr;
   int32_t* d_counts = nullptr;
@@ -541,6 +596,93 @@ int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, 
   return sync_stream(c);
 }
 
+// ---- fleet merge (RCCL) ------------------------------------------------------
+int ncclfail(l5dh_ctx* c, ncclResult_t e, const char* what) {
+  c->last_error = std::string(what) + ": " + ncclGetErrorString(e);
+  return -EIO;
+}
+
+#define NCCLCHK(c, expr)                                     \
+  do {                                                       \
+    ncclResult_t _e = (expr);                                \
+    if (_e != ncclSuccess) return ncclfail((c), _e, #expr);  \
+  } while (0)
+
+uint32_t merge_per(const l5dh_ctx* c) { return (c->S + c->nranks - 1) / c->nranks; }
+
+// Phase 1: pending samples + state -> dense rows [Sp][1798] and totals [Sp] (the
+// fused whole-range export with reset), pad rows zero.
+int merge_export(l5dh_ctx* c) {
+  if (!c->comm) return fail(c, -EINVAL, "no communicator: call l5dh_comm_init_rank or l5dh_comm_init_all first");
+  int r = flush_ring(c);
+  if (r) return r;
+  const size_t Sp = (size_t)merge_per(c) * c->nranks;
+  if ((r = ensure(c, c->merge_counts, Sp * NB * 4)) || (r = ensure(c, c->merge_totals, Sp * 8))) return r;
+  int32_t* cnt = static_cast<int32_t*>(c->merge_counts.p);
+  int64_t* tot = static_cast<int64_t*>(c->merge_totals.p);
+  if (Sp > c->S) {
+    HIPCHK(c, hipMemsetAsync(cnt + (size_t)c->S * NB, 0, (Sp - c->S) * NB * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(tot + c->S, 0, (Sp - c->S) * 8, c->stream));
+  }
+  return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot});
+}
+
+// Phase 2: the collective (callers group it across contexts).
+bool merge_skips_collective(const l5dh_ctx* c) { return c->nranks == 1 && !c->rccl_1rank; }
+
+int merge_collective(l5dh_ctx* c, int mode) {
+  if (merge_skips_collective(c)) return 0;  // one rank: the sum is the identity
+  const size_t per = merge_per(c);
+  KTimer kt(c, L5DH_K_MERGE);
+  if (mode == L5DH_MERGE_REDUCE_SCATTER) {
+    int r;
+    if ((r = ensure(c, c->recv_counts, per * NB * 4)) || (r = ensure(c, c->recv_totals, per * 8))) return r;
+    NCCLCHK(c, ncclReduceScatter(c->merge_counts.p, c->recv_counts.p, per * NB, ncclInt32, ncclSum, c->comm, c->stream));
+    NCCLCHK(c, ncclReduceScatter(c->merge_totals.p, c->recv_totals.p, per, ncclInt64, ncclSum, c->comm, c->stream));
+  } else {
+    const size_t Sp = per * c->nranks;
+    NCCLCHK(c, ncclAllReduce(c->merge_counts.p, c->merge_counts.p, Sp * NB, ncclInt32, ncclSum, c->comm, c->stream));
+    NCCLCHK(c, ncclAllReduce(c->merge_totals.p, c->merge_totals.p, Sp, ncclInt64, ncclSum, c->comm, c->stream));
+  }
+  return 0;
+}
+
+// Phase 3: summaries (+ copies) of the rows this rank received.
+int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, int64_t* totals_out, uint32_t* first,
+                 uint32_t* count) {
+  const uint32_t per = merge_per(c);
+  const bool rs = mode == L5DH_MERGE_REDUCE_SCATTER;
+  const bool recv = rs && !merge_skips_collective(c);
+  const uint32_t f = rs ? (uint32_t)std::min<uint64_t>((uint64_t)c->rank * per, c->S) : 0u;
+  const uint32_t n = rs ? std::min<uint32_t>(per, c->S - f) : c->S;
+  const int32_t* rows = static_cast<const int32_t*>(recv ? c->recv_counts.p : c->merge_counts.p);
+  const int64_t* tots = static_cast<const int64_t*>(recv ? c->recv_totals.p : c->merge_totals.p);
+  if (first) *first = f;
+  if (count) *count = n;
+  if (n == 0) return sync_stream(c);
+  int r;
+  Summary88* d_summ = nullptr;
+  const bool out_dev = out && is_device_ptr(out) && ((uintptr_t)out % 8 == 0);
+  if (out) {
+    if (out_dev)
+      d_summ = reinterpret_cast<Summary88*>(out);
+    else {
+      if ((r = ensure(c, c->stage_summ, (size_t)n * 88))) return r;
+      d_summ = static_cast<Summary88*>(c->stage_summ.p);
+    }
+    KTimer kt(c, L5DH_K_HOT);
+    HIPCHK(c, launch_rows(state(c), rows, tots, tables(c), Outputs{d_summ, nullptr, 0, n, nullptr}, 0, nullptr,
+                          c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_COPY);
+    if (out && !out_dev) HIPCHK(c, hipMemcpyAsync(out, d_summ, (size_t)n * 88, hipMemcpyDefault, c->stream));
+    if (counts_out) HIPCHK(c, hipMemcpyAsync(counts_out, rows, (size_t)n * NB * 4, hipMemcpyDefault, c->stream));
+    if (totals_out) HIPCHK(c, hipMemcpyAsync(totals_out, tots, (size_t)n * 8, hipMemcpyDefault, c->stream));
+  }
+  return sync_stream(c);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -573,8 +715,13 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   auto* c = new (std::nothrow) l5dh_ctx();
   if (!c) return -ENOMEM;
   c->device = dev;
+#ifdef L5DH_DEV
+  // development builds only (tools/mk_var.sh): timing-only kernel variants, results invalid
   if (const char* d = getenv("L5DH_DBG")) c->dbg = atoi(d);
+#endif
   c->S = max_series;
+  // staging ring: 64 samples per series, between 2^20 and 2^26 samples (4 MB .. 256 MB per array)
+  c->ring_cap = std::min<size_t>(std::max<size_t>((size_t)max_series * 64, (size_t)1 << 20), (size_t)1 << 26);
   c->F = (max_series + TILE - 1) / TILE;
   auto bail = [&](int code) {
     l5dh_close(c);
@@ -587,13 +734,13 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   // CU (LDS-bound), so a second round of slabs only adds table rows (measured: 2 x CUs
   // is ~1.4 % slower on C2 and no faster on C3)
   c->G_max = std::max(1, std::min(c->num_cu, 512));
-  if (const char* g = getenv("L5DH_GMAX")) c->G_max = std::max(1, std::min(atoi(g), 512));  // development: slab count
   if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
   if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming) != hipSuccess)
     return bail(-EIO);
   c->stream = c->own_stream;
   const size_t S = c->S, F = c->F;
@@ -601,7 +748,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
-            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)c->G_max * (F + COLS) * 4) &&
+            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)512 * (F + COLS) * 4) &&
             mal((void**)&c->d_tile_tot, (F + COLS) * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) &&
             mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
@@ -612,7 +759,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
   }
-  if (hipHostMalloc((void**)&c->h_header, 32, hipHostMallocMapped) != hipSuccess) return bail(-ENOMEM);  // header[4] + err flag
+  if (hipHostMalloc((void**)&c->h_header, 32, hipHostMallocMapped) != hipSuccess) return bail(-ENOMEM);  // header[4] + err count
+  memset(c->h_header, 0, 32);
   if (hipHostGetDevicePointer((void**)&c->h_header_dev, c->h_header, 0) != hipSuccess) return bail(-ENOMEM);
   // constant tables
   int32_t lim_pad[LIM_PAD], mid[NB], base[ROW] = {0};
@@ -659,14 +807,18 @@ int l5dh_close(l5dh_ctx* c) {
     if (s.sinfo) hipFree(s.sinfo);
     if (s.recs.p) hipFree(s.recs.p);
   }
-  DevBuf* bufs[] = {&c->scratch1, &c->hot_item, &c->split_item, &c->stage_series, &c->stage_values, &c->stage_summ, &c->stage_counts,
-                    &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals};
+  if (c->comm) ncclCommDestroy(c->comm);
+  DevBuf* bufs[] = {&c->scratch1,      &c->hot_item,        &c->split_item,   &c->stage_series, &c->stage_values,
+                    &c->stage_summ,    &c->stage_counts,    &c->stage_totals, &c->stage_in_counts,
+                    &c->stage_in_totals, &c->ring_series,   &c->ring_values,  &c->merge_counts,  &c->merge_totals,
+                    &c->recv_counts,   &c->recv_totals};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->h_header) hipHostFree(c->h_header);
   if (c->side) hipStreamDestroy(c->side);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_join) hipEventDestroy(c->ev_join);
+  if (c->ev_copy) hipEventDestroy(c->ev_copy);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return 0;
@@ -677,17 +829,8 @@ int l5dh_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
   if (n && (!series || !values)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  // batches are binned in pieces below 2^31 samples (k_bin1 tags direct-tile
-  // destinations in bit 31); an id error in one piece is reported after all pieces
-  int rc = 0;
-  for (size_t o = 0; o < n || (n == 0 && o == 0); o += MAX_BATCH) {
-    const size_t m = std::min(n - o, MAX_BATCH);
-    const int r = do_ingest(c, series + o, values + o, m);
-    if (r == -EINVAL && rc == 0 && m) rc = r;
-    else if (r) return r;
-    if (n == 0) break;
-  }
-  return rc;
+  const int r = ingest_impl(c, series, values, n);
+  return r ? r : check_err(c);
 }
 
 int l5dh_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {
@@ -703,7 +846,8 @@ int l5dh_export_state(l5dh_ctx* c, uint32_t first, uint32_t count, int32_t* coun
   hipSetDevice(c->device);
   if ((uint64_t)first + count > c->S) return fail(c, -EINVAL, "series range out of bounds");
   if (count == 0) return 0;
-  int r;
+  int r = flush_ring(c);
+  if (r) return r;
   const bool fused = full_range(c, first, count) && reset;  // the fleet merge's export: one aggregate pass
   if (!fused && (r = fold(c))) return r;
   const bool cnt_dev = counts && is_device_ptr(counts) && ((uintptr_t)counts % 8 == 0);
@@ -783,7 +927,7 @@ int l5dh_peek(l5dh_ctx* c, uint32_t series, l5dh_bucket_count* out, size_t cap, 
   hipSetDevice(c->device);
   if (series >= c->S) return fail(c, -EINVAL, "series id out of range");
   int r;
-  if ((r = fold(c))) return r;
+  if ((r = flush_ring(c)) || (r = fold(c))) return r;
   uint8_t dirty = 0;
   std::vector<uint32_t> row(ROW, 0);
   HIPCHK(c, hipMemcpyAsync(&dirty, c->d_dirty + (series >> TILE_SHIFT), 1, hipMemcpyDeviceToHost, c->stream));
@@ -814,7 +958,9 @@ int l5dh_sync(l5dh_ctx* c) {
   if (!c) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  return check_err(c);  // synchronizes the stream
+  int r;
+  if ((r = flush_ring(c)) || (r = sync_stream(c))) return r;
+  return check_err(c);
 }
 
 int l5dh_set_stream(l5dh_ctx* c, void* s) {
@@ -823,7 +969,15 @@ int l5dh_set_stream(l5dh_ctx* c, void* s) {
   hipSetDevice(c->device);
   int r = sync_stream(c);
   if (r) return r;
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  c->stream = s == L5DH_OWN_STREAM ? c->own_stream : static_cast<hipStream_t>(s);
+  return 0;
+}
+
+int l5dh_wait_event(l5dh_ctx* c, void* ev) {
+  if (!c || !ev) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  HIPCHK(c, hipStreamWaitEvent(c->stream, static_cast<hipEvent_t>(ev), 0));
   return 0;
 }
 
@@ -866,6 +1020,29 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
     case L5DH_PARAM_SPLIT_MIN:
       if (v < 1 || v > 0xFFFFFFFFll) return fail(c, -EINVAL, "split minimum must be in [1, 2^32)");
       c->split_min = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_STAGE_SAMPLES: {
+      if (v < 0 || v > (int64_t)MAX_BATCH) return fail(c, -EINVAL, "staging ring must be in [0, 2^30 - 65536] samples");
+      hipSetDevice(c->device);
+      int r = flush_ring(c);  // staged samples are binned before the ring changes size
+      if (r) return r;
+      if ((size_t)v * 4 + 64 > c->ring_series.cap) {  // the next small batch allocates the new size
+        if ((r = sync_stream(c))) return r;
+        for (DevBuf* b : {&c->ring_series, &c->ring_values}) {
+          if (b->p) hipFree(b->p);
+          b->p = nullptr;
+          b->cap = 0;
+        }
+      }
+      c->ring_cap = ((size_t)v + 3) & ~(size_t)3;
+      return 0;
+    }
+    case L5DH_PARAM_MERGE_RCCL_1RANK:
+      c->rccl_1rank = v != 0;
+      return 0;
+    case L5DH_PARAM_MAX_SLABS:
+      if (v < 1 || v > 512) return fail(c, -EINVAL, "slabs must be in [1, 512]");
+      c->G_max = (int)v;
       return 0;
     default:
       return fail(c, -EINVAL, "unknown parameter");
@@ -911,5 +1088,111 @@ int l5dh_pin_free(void* p) {
 }
 
 const char* l5dh_last_error(l5dh_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
+
+int l5dh_comm_unique_id(void* id_out) {
+  if (!id_out) return -EINVAL;
+  static_assert(sizeof(ncclUniqueId) == L5DH_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -EIO;
+  memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+
+int l5dh_comm_init_rank(l5dh_ctx* c, const void* id, int nranks, int rank) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->comm) return fail(c, -EINVAL, "context already has a communicator");
+  hipSetDevice(c->device);
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t comm = nullptr;
+  NCCLCHK(c, ncclCommInitRank(&comm, nranks, uid, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return 0;
+}
+
+int l5dh_comm_init_all(l5dh_ctx** ctxs, int n) {
+  if (!ctxs || n < 1) return -EINVAL;
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i] || ctxs[i]->comm || ctxs[i]->S != ctxs[0]->S) return -EINVAL;
+    devs[i] = ctxs[i]->device;
+  }
+  std::vector<ncclComm_t> comms(n, nullptr);
+  const ncclResult_t e = ncclCommInitAll(comms.data(), n, devs.data());
+  if (e != ncclSuccess) {
+    ctxs[0]->last_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(e);
+    return -EIO;
+  }
+  for (int i = 0; i < n; ++i) {
+    std::lock_guard<std::mutex> g(ctxs[i]->mu);
+    ctxs[i]->comm = comms[i];
+    ctxs[i]->nranks = n;
+    ctxs[i]->rank = i;
+  }
+  return 0;
+}
+
+int l5dh_comm_destroy(l5dh_ctx* c) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->comm) {
+    hipSetDevice(c->device);
+    int r = sync_stream(c);
+    if (r) return r;
+    ncclCommDestroy(c->comm);
+  }
+  c->comm = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+  return 0;
+}
+
+int l5dh_merge(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, int64_t* totals_out, uint32_t* first,
+               uint32_t* count) {
+  if (!c || (mode != L5DH_MERGE_REDUCE_SCATTER && mode != L5DH_MERGE_ALL_REDUCE)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r;
+  if ((r = merge_export(c))) return r;
+  NCCLCHK(c, ncclGroupStart());
+  r = merge_collective(c, mode);
+  const ncclResult_t ge = ncclGroupEnd();
+  if (r) return r;
+  if (ge != ncclSuccess) return ncclfail(c, ge, "ncclGroupEnd");
+  return merge_finish(c, mode, out, counts_out, totals_out, first, count);
+}
+
+int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_t** counts_outs, int64_t** totals_outs,
+                   uint32_t* firsts, uint32_t* counts) {
+  if (!ctxs || n < 1 || (mode != L5DH_MERGE_REDUCE_SCATTER && mode != L5DH_MERGE_ALL_REDUCE)) return -EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (!ctxs[i] || !ctxs[i]->comm || ctxs[i]->nranks != n || ctxs[i]->rank != i) return -EINVAL;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (int i = 0; i < n; ++i) locks.emplace_back(ctxs[i]->mu);  // in rank order
+  int r;
+  for (int i = 0; i < n; ++i) {
+    hipSetDevice(ctxs[i]->device);
+    if ((r = merge_export(ctxs[i]))) return r;
+  }
+  NCCLCHK(ctxs[0], ncclGroupStart());
+  for (int i = 0; i < n && !r; ++i) {
+    hipSetDevice(ctxs[i]->device);
+    r = merge_collective(ctxs[i], mode);
+  }
+  const ncclResult_t ge = ncclGroupEnd();
+  if (r) return r;
+  if (ge != ncclSuccess) return ncclfail(ctxs[0], ge, "ncclGroupEnd");
+  for (int i = 0; i < n; ++i) {
+    hipSetDevice(ctxs[i]->device);
+    if ((r = merge_finish(ctxs[i], mode, outs ? outs[i] : nullptr, counts_outs ? counts_outs[i] : nullptr,
+                          totals_outs ? totals_outs[i] : nullptr, firsts ? firsts + i : nullptr,
+                          counts ? counts + i : nullptr)))
+      return r;
+  }
+  return 0;
+}
 
 }  // extern "C"

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ serie
       hot_inc(cnt, ok ? count_key(s, F, sw[s >> (TILE_SHIFT + 5)]) : 0u, ok, hk[0], hk[1]);
     }
   }
-  if (bad) atomicOr(err, 1u);
+  if (bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
   __syncthreads();
   uint32_t* row = table + (size_t)blockIdx.x * C;
   for (uint32_t t = threadIdx.x; t < C; t += WG) row[t] = cnt[t];

@@ -73,21 +73,35 @@ class StatEngine:
         self.batch = int(batch)
         self._lock = threading.Lock()
         self._next = 0
+        self._free: List[int] = []
+        self._limits = None
         self._tls = threading.local()
         self._buffers: List["_Staging"] = []
 
-    # registry (MetricsTree.mkStat assigns the id)
+    # registry (MetricsTree.mkStat assigns the id; MetricsTree.prune releases it)
     def register(self) -> int:
         with self._lock:
+            if self._free:
+                return self._free.pop()
             if self._next >= self.capacity:
                 raise RuntimeError(f"histogram engine full: {self.capacity} series")
             sid = self._next
             self._next += 1
             return sid
 
+    def release(self, sid: int) -> None:
+        """Return a pruned Stat's id (MetricsPruningModule.scala:14-39 prunes closed
+        clients' subtrees).  Its staged samples are flushed and its row is cleared
+        on the GPU before the id can be handed out again, so a new Stat starts empty."""
+        self.flush()
+        self.engine.snapshot(first=sid, count=1, reset=True)
+        with self._lock:
+            self._free.append(sid)
+
     @property
     def registered(self) -> int:
-        return self._next
+        """Series ids currently held by Stats."""
+        return self._next - len(self._free)
 
     def _staging(self) -> "_Staging":
         st = getattr(self._tls, "st", None)
@@ -128,6 +142,20 @@ class StatEngine:
     def peek(self, sid: int) -> List[BucketAndCount]:
         self.flush()
         return [BucketAndCount(int(b["lower"]), int(b["upper"]), int(b["count"])) for b in self.engine.peek(sid)]
+
+    def reset_series(self, sid: int) -> List[BucketAndCount]:
+        """Metric.Stat.reset (Metric.scala:44-51): bucketAndCounts + clear as ONE
+        engine call (snapshot of one series with its counts and reset), so no sample
+        flushed by another thread can fall between the two."""
+        self.flush()
+        _, counts = self.engine.snapshot(first=sid, count=1, reset=True, with_counts=True)
+        if self._limits is None:
+            from . import _native
+            self._limits = _native.limits()
+        L = self._limits
+        row = counts[0]
+        return [BucketAndCount(0 if b == 0 else int(L[b - 1]), int(L[b]) if b < len(L) else 2147483647, int(row[b]))
+                for b in np.flatnonzero(row > 0)]
 
     def snapshot_all(self, reset: bool = True) -> np.ndarray:
         """Summaries of every series in one fused GPU pass (snapshot + reset)."""
@@ -186,10 +214,20 @@ class Metric:
             return self._reset_time
 
         def add(self, value: float) -> None:
+            if self.series_id is None and self._engine is not None:
+                return  # pruned: like adding to a histogram no exporter reads any more
             self._eng().add(self.series_id, value)
 
         def peek(self) -> List[BucketAndCount]:
+            if self.series_id is None and self._engine is not None:
+                return []
             return self._eng().peek(self.series_id)
+
+        def _release(self) -> None:
+            """MetricsTree.prune: hand the series id back to the engine."""
+            sid, self.series_id = self.series_id, None
+            if self._engine is not None and sid is not None:
+                self._engine.release(sid)
 
         def snapshot(self) -> HistogramSummary:
             self._summary_snapshot = self.summary
@@ -197,8 +235,7 @@ class Metric:
 
         def reset(self) -> Tuple[List[BucketAndCount], float]:
             eng = self._eng()
-            buckets = eng.peek(self.series_id)
-            eng.summary(self.series_id, reset=True)
+            buckets = [] if self.series_id is None else eng.reset_series(self.series_id)
             now = time.time()
             delta = now - self._reset_time
             self._reset_time = now
@@ -206,6 +243,8 @@ class Metric:
 
         @property
         def summary(self) -> HistogramSummary:
+            if self.series_id is None and self._engine is not None:
+                return HistogramSummary(0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0.0)
             return self._eng().summary(self.series_id, reset=False)
 
         @property
@@ -319,7 +358,9 @@ class MetricsTree:
         for k in kids:
             k.prune()
         with self._mlock:
-            self._metric = Metric.NONE
+            m, self._metric = self._metric, Metric.NONE
+        if isinstance(m, Metric.Stat):
+            m._release()
 
     def walk(self, prefix: Tuple[str, ...] = ()):
         """Depth-first (path, tree) pairs."""

@@ -57,7 +57,7 @@ def test_header_constants_match_host():
 
     assert define("L5DH_NLIMITS") == N.NLIMITS == 1797
     assert define("L5DH_NBUCKETS") == N.NBUCKETS == 1798
-    assert define("L5DH_ABI_VERSION") == 1
+    assert define("L5DH_ABI_VERSION") == 2
     enum = dict((k, int(v)) for k, v in re.findall(r"(L5DH_(?:PARAM|K)_[A-Z0-9_]+) = (\d+)", h))
     assert enum["L5DH_PARAM_TIMING"] == N.PARAM_TIMING
     assert enum["L5DH_PARAM_COLD_LIMIT"] == N.PARAM_COLD_LIMIT
@@ -73,7 +73,7 @@ def test_header_constants_match_host():
 
 
 def test_abi_version_and_limits(lib, oracle):
-    assert lib.l5dh_abi_version() == 1
+    assert lib.l5dh_abi_version() == 2
     lim = N.limits()
     assert lim.dtype == np.int32 and lim.shape == (N.NLIMITS,)
     np.testing.assert_array_equal(lim, oracle.limits())

@@ -104,7 +104,7 @@ def test_escape_label_val_rule():
 def test_java_number_strings():
     assert [double_to_string(x) for x in (1.0, 1.5, 3030.0, 1e7, 1e-4, 281.7352941176471, 0.0)] == \
         ["1.0", "1.5", "3030.0", "1.0E7", "1.0E-4", "281.7352941176471", "0.0"]
-    assert float_to_string(4008938.8) == "4008938.8" and float_to_string(1.48832833e12) == "1.4883283E12"
+    assert float_to_string(4008938.8) == "4008938.8" and float_to_string(1.48832833e12) == "1.48832833E12"  # JDK 8 (tests/test_javafmt.py)
 
 
 def test_line_multiset_compare():

@@ -40,6 +40,9 @@ def main(d, out_json=None, meta=None):
         print(k, json.dumps({c: (round(v / 1e6, 2) if "bytes" in c else round(v)) for c, v in row.items()}))
     if out_json:
         doc = dict(meta or {})
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        from linkerd_amd._native import engine_source_hash
+        doc["src_hash"] = engine_source_hash()  # bench.py marks the traffic stale when the sources change
         doc["kernels"] = res
         json.dump(doc, open(out_json, "w"), indent=1)
 
