@@ -286,6 +286,9 @@ def run(args):
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    # one non-default stream for the generator, torch and the engine (l5dh_set_stream):
+    # device inputs and outputs are then stream ordered, no host wait per ingest
+    torch.cuda.set_stream(torch.cuda.Stream())
 
     from linkerd_amd import _native as N_
     from linkerd_amd.engine import HistogramEngine
@@ -317,6 +320,7 @@ def run(args):
     rows = eng.merge_rows() if fleet else S
     summ = torch.empty((max(rows, 1), 11), dtype=torch.int64, device=dev)
     counts = None if fleet else torch.empty((max(S, 1), N_.NBUCKETS), dtype=torch.int32, device=dev)
+    eng.set_stream(stream)
 
     host = None
     if streaming:  # the batch in pinned host memory (l5dh_pin_alloc, what the JNI side stages into)

@@ -365,11 +365,22 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, c->hot_chunk, c->d_dirty, pl, c->stream));
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // the plan kernel wrote h_header (mapped pinned memory)
-  const uint32_t cold_items = c->h_header[0];
-  const uint32_t hot = c->h_header[1];
-  const uint32_t hot_items = c->h_header[2];
-  const uint32_t split_items = c->h_header[3];
+  // The accumulate kernels are persistent and read their item counts from the plan
+  // header on the device, so no host round trip separates them from the plan: the
+  // launches get upper bounds (a hot tile holds > cold_limit records).
+  size_t recs = 0;
+  for (int j = 0; j < c->nseg; ++j) recs += c->segs[j].n;
+  uint32_t cold_items = DEV_COUNT;
+  uint32_t hot = (uint32_t)std::min<size_t>(c->F, recs / ((size_t)c->cold_limit + 1));
+  uint32_t hot_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / c->hot_chunk + hot);
+  uint32_t split_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / c->hot_chunk + 2 * (size_t)hot);
+  if (c->dbg) {  // development builds: the timing variants take exact host counts
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the plan kernel wrote h_header (mapped pinned memory)
+    cold_items = c->h_header[0];
+    hot = c->h_header[1];
+    hot_items = c->h_header[2];
+    split_items = c->h_header[3];
+  }
   State st = state(c);
   Tables tb = tables(c);
   if (hot) {

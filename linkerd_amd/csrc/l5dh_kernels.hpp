@@ -156,13 +156,17 @@ hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, co
                        const uint32_t* stplan, uint32_t* records, int dbg, hipStream_t st);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
                        const uint8_t* dirty, Plan plan, hipStream_t st);
-hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st);
-hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
+// The accumulate launches take UPPER BOUNDS of their item counts (no host round
+// trip for the plan header): the kernels are persistent and read the exact counts
+// from plan.header on the device.  DEV_COUNT as a count: read it on the device.
+constexpr uint32_t DEV_COUNT = 0xFFFFFFFFu;
+hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, uint32_t hot_chunk, hipStream_t st);
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st);
-hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t split_items, State state, Tables tb, uint32_t hot_chunk,
-                              hipStream_t st);
-hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
+hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
+                              uint32_t hot_chunk, hipStream_t st);
+hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
                              int reset, uint32_t hot_chunk, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external
 // dense rows ext[count][1798] + ext_total[count].

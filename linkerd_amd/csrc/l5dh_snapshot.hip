@@ -215,15 +215,19 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
 
 // k_hot_init: split tiles accumulate with global atomics into state rows, so
 // clean ones start from zero.
+// Persistent (the number of hot tiles, header[1], is read on the device).
 __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t hot_chunk) {
-  const uint32_t t = plan.hot_list[blockIdx.x];
-  if (st.dirty[t] || (plan.tile_flags[t] & TF_SINGLE)) return;  // single-chunk tiles emit in place
-  const uint32_t s0 = t * TILE;
-  const uint32_t s1 = min(st.S, s0 + TILE);
-  uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
-  const size_t n4 = (size_t)(s1 - s0) * ROW / 4;
-  for (size_t i = threadIdx.x; i < n4; i += 256) p[i] = make_uint4(0, 0, 0, 0);
-  if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
+  const uint32_t nh = plan.header[1];
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const uint32_t t = plan.hot_list[i];
+    if (st.dirty[t] || (plan.tile_flags[t] & TF_SINGLE)) continue;  // single-chunk tiles emit in place
+    const uint32_t s0 = t * TILE;
+    const uint32_t s1 = min(st.S, s0 + TILE);
+    uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
+    const size_t n4 = (size_t)(s1 - s0) * ROW / 4;
+    for (size_t k = threadIdx.x; k < n4; k += 256) p[k] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
+  }
 }
 
 struct SrcLds32 {  // u32 row in LDS (half-tiles of big tiles), bins 1798/1799 zero
@@ -496,8 +500,9 @@ __global__ __launch_bounds__(NT, 4) void k_accum_cold(Segs segs, Plan plan, Stat
 // emission, so their latency hides behind it (and behind its dense stores).
 template <int NSER, int NT>
 __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                      uint32_t cold_items, int final_mode, int reset) {
+                                                      uint32_t cold_arg, int final_mode, int reset) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t cold_items = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
   uint32_t* hist = smem;                                      // [NSER][900] u16 pairs
   uint32_t* vsl = smem + NSER * CROW;                         // [NSER][64] lane-private value sums
   uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
@@ -664,8 +669,11 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
                                                   int reset) {
   (void)cold_limit;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t p = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);  // chunk item
-  const uint32_t half = (blockIdx.x / 8) & 1u;
+  // persistent: virtual blocks vb = blockIdx.x + r * gridDim.x (gridDim.x a multiple of
+  // 16, so both halves of a chunk item stay 8 blocks apart); p grows with r
+  for (uint32_t vb = blockIdx.x;; vb += gridDim.x) {
+  const uint32_t p = (vb / 16) * 8 + (vb % 8);  // chunk item
+  const uint32_t half = (vb / 8) & 1u;
   if (p >= plan.header[2]) return;
   const uint32_t hx = plan.hot_item[p];
   const uint32_t t = hx & 0x7FFFu;
@@ -719,6 +727,8 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   }
   // dirty[t] of a single-chunk tile is updated by k_hot_finish: the other half may
   // not have read it yet.
+  __syncthreads();  // the LDS rows are read: the next item may clear them
+  }
 }
 
 // Split big tiles (split in every pending segment): item = (tile, half, chunk of
@@ -729,7 +739,9 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
 // cleared the rows; k_hot_finish summarizes them).
 __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint2 it = plan.split_item[blockIdx.x];
+  const uint32_t nitems = plan.header[3];  // persistent: items blockIdx.x, + gridDim.x, ...
+  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+  const uint2 it = plan.split_item[item];
   const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
@@ -791,17 +803,21 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
     }
     if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
   }
+  __syncthreads();  // the LDS rows are read: the next item may clear them
+  }
 }
 
 // k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
 // write outputs, update state/dirty.
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
                                                    int reset, uint32_t hot_chunk) {
-  const uint32_t t = plan.hot_list[blockIdx.x >> 1];
-  const uint32_t half = blockIdx.x & 1u;
+  const uint32_t nv = 2 * plan.header[1];  // persistent: (hot tile, half) pairs
+  for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
+  const uint32_t t = plan.hot_list[vb >> 1];
+  const uint32_t half = vb & 1u;
   if (plan.tile_flags[t] & TF_SINGLE) {  // emitted by k_accum_hot
     if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
-    return;
+    continue;
   }
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
@@ -824,6 +840,7 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
     }
   }
   if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
+  }
 }
 
 // k_rows: one wave per series: summary / dense copy of state rows (range
@@ -914,34 +931,41 @@ hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limi
   return hipGetLastError();
 }
 
-hipError_t launch_hot_init(Plan plan, uint32_t num_hot, State state, uint32_t hot_chunk, hipStream_t st) {
-  if (num_hot == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hot_init, dim3(num_hot), dim3(256), 0, st, plan, state, hot_chunk);
+static int num_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+
+hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, uint32_t hot_chunk, hipStream_t st) {
+  if (max_hot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hot_init, dim3(std::min<uint32_t>(max_hot, 4u * num_cus())), dim3(256), 0, st, plan, state,
+                     hot_chunk);
   return hipGetLastError();
 }
 
-hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_items, State state, Tables tb,
+hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
                         hipStream_t st) {
+  const uint32_t ncu = (uint32_t)num_cus();
   if (cold_items) {
     // default: the persistent form, one 1024-thread workgroup per CU walking the cold
-    // tiles (-3 % against a workgroup per tile, measured).  L5DH_DBG bit 0x800000: a
-    // workgroup per tile; with bit 0x20000 also: half-tile items, two 512-thread
-    // workgroups per CU (measured slower, alone and next to the split items)
+    // tiles (-3 % against a workgroup per tile, measured); cold_items may be DEV_COUNT
+    // (read on the device).  Development builds (L5DH_DBG, host counts only): bit
+    // 0x800000 a workgroup per tile, with 0x20000 half-tile items; bit 0x2000000 the
+    // persistent half-tile form (all measured slower)
     if (!(g_dbg_host & 0x800000)) {
-      static int ncu = 0;
-      if (!ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-          ncu = 256;
-      }
-      if (g_dbg_host & 0x2000000) {  // bit 0x2000000: half-tile items, two 512-thread workgroups per CU
-        const uint32_t pairs = std::min<uint32_t>(cold_items, (uint32_t)ncu);
+      if (g_dbg_host & 0x2000000) {
+        const uint32_t pairs = std::min<uint32_t>(cold_items, ncu);
         hipLaunchKernelGGL((k_accum_cold_p<16, 512>), dim3(((pairs + 7) / 8) * 16), dim3(512), acc_cold_p_lds(16), st,
                            segs, plan, state, tb, out, cold_items, final_mode, reset);
       } else {
-        const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)ncu);
+        const uint32_t grid = std::min<uint32_t>(cold_items, ncu);
         hipLaunchKernelGGL((k_accum_cold_p<32, 1024>), dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan,
                            state, tb, out, cold_items, final_mode, reset);
       }
@@ -954,8 +978,8 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (hot_items) {
-    const uint32_t blocks = ((2 * hot_items + 15) / 16) * 16;  // (chunk, half) pairs 8 blocks apart
+  if (max_hot_items) {  // persistent: (chunk, half) pairs 8 blocks apart, a multiple of 16 blocks
+    const uint32_t blocks = ((std::min<uint32_t>(2 * max_hot_items, 2 * ncu) + 15) / 16) * 16;
     hipLaunchKernelGGL(k_accum_hot, dim3(blocks), dim3(WG), ACC_HOT_LDS, st, segs, plan, state, tb, out, cold_limit,
                        hot_chunk, final_mode, reset);
     return hipGetLastError();
@@ -963,18 +987,19 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t hot_
   return hipSuccess;
 }
 
-hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t split_items, State state, Tables tb, uint32_t hot_chunk,
-                              hipStream_t st) {
-  if (split_items == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_accum_split, dim3(split_items), dim3(WG), ACC_SPLIT_LDS, st, segs, plan, state, tb, hot_chunk);
+hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
+                              uint32_t hot_chunk, hipStream_t st) {
+  if (max_split_items == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, (uint32_t)num_cus())), dim3(WG),
+                     ACC_SPLIT_LDS, st, segs, plan, state, tb, hot_chunk);
   return hipGetLastError();
 }
 
-hipError_t launch_hot_finish(Plan plan, uint32_t num_hot, State state, Tables tb, Outputs out, int final_mode,
+hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
                              int reset, uint32_t hot_chunk, hipStream_t st) {
-  if (num_hot == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hot_finish, dim3(num_hot * 2), dim3(WG), 0, st, plan, state, tb, out, final_mode, reset,
-                     hot_chunk);
+  if (max_hot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hot_finish, dim3(std::min<uint32_t>(2 * max_hot, 2u * num_cus())), dim3(WG), 0, st, plan, state,
+                     tb, out, final_mode, reset, hot_chunk);
   return hipGetLastError();
 }
 
