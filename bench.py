@@ -57,11 +57,16 @@ KERNEL_ALG_BYTES = {
     "accum": lambda n, s, fleet: (7192 if fleet else 7280) * s,  # writes counts (+ summary)
 }
 METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
-# device cost model of one step on MI355X, for the C3 shard plan (round-2 kernel
-# times: C3 ingest 5.25 ms / 1e9 samples + accumulate ~1.3 ps per record; a 241K-
-# series shard accumulates in 0.41 ms; profiles/r02_*_bench.json)
+# device cost model of one step on MI355X, for the C3 shard plan: a base model
+# (COST_PS_PER_SAMPLE per Zipf-expected sample + COST_PS_PER_SERIES per series row)
+# times a measured correction per Zipf-rank range -- each range's measured shard
+# time over its base-model time, from the 8 single-GPU runs of `--shard r/8`
+# (profiles/r02b_shards.jsonl): direct tiles, split tiles through level 2 and
+# cold tiles cost differently per sample
 COST_PS_PER_SAMPLE = 6.5
 COST_PS_PER_SERIES = 1700.0
+COST_CALIBRATION = ((0, 1.195), (5, 1.041), (53, 0.915), (508, 1.048), (4832, 1.341), (40831, 1.191),
+                    (209433, 1.219), (553969, 1.180))  # (first Zipf rank, ms of that r/8 shard)
 
 
 def parse():
@@ -121,8 +126,7 @@ def plan(args, world: int, rank: int) -> dict:
         # balanced by expected device time: COST_PS_PER_SAMPLE per Zipf-expected
         # sample + COST_PS_PER_SERIES per series row (balancing by samples alone
         # would leave the last rank most of the dense series rows)
-        pmf = np.diff(np.concatenate([[0.0], cdf]))
-        shards = fleet.shard_ranges(S, world, weights=COST_PS_PER_SAMPLE * N * pmf + COST_PS_PER_SERIES)
+        shards = fleet.shard_ranges(S, world, weights=shard_cost(cdf, N))
         sh = shards[rank]
         mass = [float(cdf[x.first + x.count - 1] - (cdf[x.first - 1] if x.first else 0.0)) if x.count else 0.0
                 for x in shards]
@@ -138,6 +142,19 @@ def plan(args, world: int, rank: int) -> dict:
         S, N = args.series or 1, args.samples or 10_000_000
     return dict(workload=wl, S_total=S * world, N_total=N * world, first=rank * S, count=S, samples=N,
                 base_index=0, world=world, rank=rank, scaling="weak")
+
+
+def shard_cost(cdf, N):
+    """Expected device time per series of the C3 workload (COST_* above)."""
+    import numpy as np
+    S = cdf.size
+    pmf = np.diff(np.concatenate([[0.0], cdf]))
+    w = COST_PS_PER_SAMPLE * N * pmf + COST_PS_PER_SERIES
+    if S == S_C3 and N == N_C3:  # the calibration is of this workload
+        edges = [a for a, _ in COST_CALIBRATION] + [S]
+        for (a, ms), b in zip(COST_CALIBRATION, edges[1:]):
+            w[a:b] *= ms / w[a:b].sum()
+    return w
 
 
 def gen_batch(torch, synth_lib, pl, seed_off, stream):

@@ -205,6 +205,7 @@ struct l5dh_ctx {
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
   uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
+  bool hot_slots = true;             // k_bin1 counts a bin holding >= half the batch in lane-private slots
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // staging ring: small ingest batches are concatenated on the device and binned together
   DevBuf ring_series, ring_values;
@@ -490,7 +491,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
       HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
                               (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
-                              ((c->dbg >> 20) & 1) || ((c->dbg >> 22) & 1),  // k_bin1 variants with hot slots
+                              // hot k_bin1 bins: always (bit 0), auto lane-private slots (bit 1)
+                              1 | (c->hot_slots ? 2 : 0),
                               c->stream));
       c->split_cur ^= 1;
     }

@@ -138,6 +138,7 @@ constexpr int PLAN_DPRE = 3072;     // [1024] direct tiles before word w
 constexpr int PLAN_DLIST = 4096;    // [256] direct tile ids, ascending
 constexpr int PLAN_DSI = 4352;      // [256] their split index
 constexpr int PLAN_ND = 4608;       // number of direct tiles
+constexpr int PLAN_HS = 4609;       // 1: one k_bin1 bin holds >= half the batch (lane-private hot slots pay)
 constexpr int PLAN_SPLIT = 8192;    // two split-set slots (this batch's, the next batch's)
 constexpr int PLAN_WORDS = PLAN_SPLIT + 2 * SPLIT_SLOT;
 // Super-tile plan (level-2 items, direct bins, hot keys) for this batch's split

@@ -30,10 +30,12 @@ def test_c3_ranks_cover_the_series_space(gpus):
         assert b["base_index"] == a["base_index"] + a["samples"]
     assert plans[-1]["first"] + plans[-1]["count"] == 1_000_000
     assert sum(p["samples"] for p in plans) == 1_000_000_000
-    # equal modelled device time per rank (bench.COST_PS_PER_SAMPLE / _SERIES), within 2 %
+    # equal modelled device time per rank (bench.shard_cost), within 2 %
     sys.path.insert(0, REPO)
     import bench
-    cost = [bench.COST_PS_PER_SAMPLE * p["samples"] + bench.COST_PS_PER_SERIES * p["count"] for p in plans]
+    from linkerd_amd import synth
+    w = bench.shard_cost(synth.zipf_cdf(1_000_000), 1_000_000_000)
+    cost = [w[p["first"]:p["first"] + p["count"]].sum() for p in plans]
     assert max(cost) / min(cost) < 1.02
 
 
