@@ -42,6 +42,10 @@ def shard_ranges(total_series: int, world: int, weights: Optional[np.ndarray] = 
         c = np.concatenate([[0.0], np.cumsum(w)])
         targets = c[-1] * np.arange(world + 1) / world
         bounds = np.searchsorted(c, targets, side="left").tolist()
+        for r in range(1, world):  # the nearer of the two boundaries around the target
+            b = bounds[r]
+            if 0 < b <= total_series and targets[r] - c[b - 1] < c[b] - targets[r]:
+                bounds[r] = b - 1
         bounds[0], bounds[-1] = 0, total_series
         for r in range(1, world + 1):  # monotone, every rank may own zero or more
             bounds[r] = max(bounds[r], bounds[r - 1])
@@ -70,19 +74,32 @@ def padded_rows(S: int, world: int) -> int:
     return ((S + world - 1) // world) * world
 
 
-def fleet_merge(counts, totals, group=None, mode: str = "reduce_scatter"):
+def alloc_dense(S: int, world: int, device=None):
+    """Dense merge buffers with padded_rows(S, world) rows (pad rows zero): export
+    into counts[:S] / totals[:S] and pass the padded tensors to fleet_merge, which
+    then reduces them in place of a padded copy."""
+    import torch
+    Sp = padded_rows(S, world)
+    return (torch.zeros((Sp, NB), dtype=torch.int32, device=device),
+            torch.zeros(Sp, dtype=torch.int64, device=device))
+
+
+def fleet_merge(counts, totals, group=None, mode: str = "reduce_scatter", S: Optional[int] = None):
     """Sum per-rank dense state across ranks.
 
     counts: torch int32 [S][1798], totals: torch int64 [S] (same S on every rank;
-    device tensors with RCCL, CPU tensors with gloo).  Returns (counts_slice,
-    totals_slice, first): the rows this rank owns after the merge (all rows for
-    mode="all_reduce")."""
+    device tensors with RCCL, CPU tensors with gloo), or the padded buffers of
+    alloc_dense (pass the series count as S; no copy is made then).  Returns
+    (counts_slice, totals_slice, first): the rows this rank owns after the merge
+    (all rows for mode="all_reduce").  The engine's own merge is l5dh_merge
+    (HistogramEngine.merge): RCCL inside the library; this is the same exchange
+    over torch.distributed, kept for the gloo tests."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    S = counts.shape[0]
+    S = counts.shape[0] if S is None else int(S)
     if mode == "all_reduce":
         dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
         dist.all_reduce(totals, op=dist.ReduceOp.SUM, group=group)
@@ -91,9 +108,9 @@ def fleet_merge(counts, totals, group=None, mode: str = "reduce_scatter"):
         raise ValueError(f"unknown merge mode {mode!r}")
     Sp = padded_rows(S, world)
     per = Sp // world
-    if Sp != S:
-        counts = torch.cat([counts, counts.new_zeros((Sp - S, NB))])
-        totals = torch.cat([totals, totals.new_zeros(Sp - S)])
+    if counts.shape[0] != Sp:  # not alloc_dense buffers: one padded copy
+        counts = torch.cat([counts, counts.new_zeros((Sp - counts.shape[0], NB))])
+        totals = torch.cat([totals, totals.new_zeros(Sp - totals.shape[0])])
     if dist.get_backend(group) == "gloo":
         # gloo has no reduce_scatter: all_reduce and keep this rank's slice
         dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
