@@ -205,7 +205,8 @@ struct l5dh_ctx {
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
   uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
-  bool hot_slots = true;             // k_bin1 counts a bin holding >= half the batch in lane-private slots
+  bool hot_slots = false;            // k_bin1: lane-private slots for a bin holding >= half the batch (superseded
+                                     // by the ballot ranking of the two hottest bins; measured slower)
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // staging ring: small ingest batches are concatenated on the device and binned together
   DevBuf ring_series, ring_values;

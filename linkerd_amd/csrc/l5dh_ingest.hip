@@ -333,6 +333,8 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
   // batch (a single-series or few-series shard: every lane of a wave would otherwise
   // serialize on one LDS counter); on C3's 23 % bin they measured 5-8 % slower
   const bool HS = HS_ALWAYS || plan[PLAN_HS] != 0u;
+  // the batch's two hottest bins (ranked by wave ballots; NOKEY: none)
+  const uint32_t hb0 = plan[3 * FS + 1], hb1 = plan[3 * FS + 2];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint32_t TB = FS + 2 * ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
@@ -462,9 +464,39 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         }
       } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
+        for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
+    }
+    if (!HS) {
+      // ranks: the batch's two hottest bins (k_stplan; e.g. a Zipf head's direct tile,
+      // ~1/4 of C3) by wave ballots -- one LDS atomic per wave and bin for all PT
+      // slots, and consecutive stage slots for a wave's hot samples -- the other bins
+      // by one LDS atomic per slot.  Same-address atomics on a hot counter otherwise
+      // serialize (SQ_LDS_ADDR_CONFLICT) and their scattered stage slots conflict.
+      uint32_t wc0 = 0, wc1 = 0;
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint32_t b = pk[k] >> 14;
+        const bool m0 = b == hb0, m1 = b == hb1;
+        wc0 += (uint32_t)__popcll(__ballot(m0));
+        wc1 += (uint32_t)__popcll(__ballot(m1));
+        if (!m0 && !m1) pk[k] |= atomicAdd(cnt + b, 1u);
+      }
+      uint32_t base = 0;
+      if (lane == 0 && wc0) base = atomicAdd(cnt + hb0, wc0);
+      if (lane == 1 && wc1) base = atomicAdd(cnt + hb1, wc1);
+      uint32_t r0 = __builtin_amdgcn_readlane(base, 0), r1 = __builtin_amdgcn_readlane(base, 1);
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint32_t b = pk[k] >> 14;
+        const bool m0 = b == hb0, m1 = b == hb1;
+        const unsigned long long x0 = __ballot(m0), x1 = __ballot(m1);
+        if (m0) pk[k] |= r0 + mask_below(x0);
+        if (m1) pk[k] |= r1 + mask_below(x1);
+        r0 += (uint32_t)__popcll(x0);
+        r1 += (uint32_t)__popcll(x1);
+      }
     }
     if (L5DH_EXP & 16) {  // timing: loads + ranking only (no scan, scatter or run writes)
       uint32_t x = 0;
