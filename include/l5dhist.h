@@ -73,7 +73,9 @@ enum {
   L5DH_PARAM_SPLIT_MIN = 8,    /* tiles laid out per half-tile have >= this many records per batch */
   L5DH_PARAM_STAGE_SAMPLES = 9, /* device staging ring for small batches, in samples (0: off) */
   L5DH_PARAM_MAX_SLABS = 10,   /* ingest slabs (workgroups of the partition kernels), 1..512 */
-  L5DH_PARAM_MERGE_RCCL_1RANK = 11 /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
+  L5DH_PARAM_MERGE_RCCL_1RANK = 11, /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
+  L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
+                                  every variant computes the same results) */
 };
 
 /* Fleet-merge modes for l5dh_merge */

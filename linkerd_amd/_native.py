@@ -37,6 +37,7 @@ PARAM_SPLIT_MIN = 8
 PARAM_STAGE_SAMPLES = 9
 PARAM_MAX_SLABS = 10
 PARAM_MERGE_RCCL_1RANK = 11
+PARAM_VARIANT = 12
 
 MERGE_REDUCE_SCATTER = 0
 MERGE_ALL_REDUCE = 1

@@ -218,7 +218,8 @@ struct l5dh_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf merge_counts, merge_totals, recv_counts, recv_totals;
-  bool rccl_1rank = false;  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
+  bool rccl_1rank = false;
+  uint32_t variant = 0;  // L5DH_PARAM_VARIANT: result-preserving kernel variants (A/B timing)  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
   uint32_t hot_chunk = 1u << 18;  // records per big-tile item (u32 LDS bins, one half-tile per workgroup)
@@ -501,7 +502,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
                             c->d_tile_tot, cur, static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
-                            c->dbg, c->stream));
+                            c->dbg | (int)(c->variant << 27), c->stream));
     }
     KTimer kt(c, L5DH_K_BIN2);
     HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, c->d_tile_tot,
@@ -1051,6 +1052,10 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->ring_cap = ((size_t)v + 3) & ~(size_t)3;
       return 0;
     }
+    case L5DH_PARAM_VARIANT:
+      if (v < 0 || v > 15) return fail(c, -EINVAL, "variant bits must be in [0, 15]");
+      c->variant = (uint32_t)v;
+      return 0;
     case L5DH_PARAM_MERGE_RCCL_1RANK:
       c->rccl_1rank = v != 0;
       return 0;

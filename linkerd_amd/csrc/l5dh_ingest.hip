@@ -463,12 +463,17 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
           pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
         }
       } else {
+        if ((dbg >> 27) & 1) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
+          for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
+        }
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
-    if (!HS) {
+    if (!HS && !((dbg >> 27) & 1)) {  // (variant bit 0: every bin by LDS atomics)
       // ranks: the batch's two hottest bins (k_stplan; e.g. a Zipf head's direct tile,
       // ~1/4 of C3) by wave ballots -- one LDS atomic per wave and bin for all PT
       // slots, and consecutive stage slots for a wave's hot samples -- the other bins
