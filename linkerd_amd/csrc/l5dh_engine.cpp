@@ -205,8 +205,6 @@ struct l5dh_ctx {
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
   uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
-  bool hot_slots = false;            // k_bin1: lane-private slots for a bin holding >= half the batch (superseded
-                                     // by the ballot ranking of the two hottest bins; measured slower)
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // staging ring: small ingest batches are concatenated on the device and binned together
   DevBuf ring_series, ring_values;
@@ -493,8 +491,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
       HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
                               (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
-                              // hot k_bin1 bins: always (bit 0), auto lane-private slots (bit 1)
-                              1 | (c->hot_slots ? 2 : 0),
+                              1,  // the hot k_bin1 bins (ballot ranking when one holds >= half)
                               c->stream));
       c->split_cur ^= 1;
     }

@@ -329,12 +329,15 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t NW = (F + 31) / 32;
   const uint32_t ND = plan[PLAN_ND];
-  // lane-private counters for the hottest bins: only when one bin holds >= half the
-  // batch (a single-series or few-series shard: every lane of a wave would otherwise
-  // serialize on one LDS counter); on C3's 23 % bin they measured 5-8 % slower
-  const bool HS = HS_ALWAYS || plan[PLAN_HS] != 0u;
-  // the batch's two hottest bins (ranked by wave ballots; NOKEY: none)
-  const uint32_t hb0 = plan[3 * FS + 1], hb1 = plan[3 * FS + 2];
+  // lane-private counters for the hottest bins (development variant, HS_ALWAYS)
+  const bool HS = HS_ALWAYS;
+  // When one bin holds >= half the batch (a single-series or few-series shard: every
+  // lane of a wave would otherwise serialize on its LDS counter), the batch's two
+  // hottest bins are ranked by wave ballots; measured (tools/ab_var.py, same context):
+  // 41 % faster on C3's first 8-way shard, 2 % slower on C3 (hottest bin 23 %), 17 %
+  // slower on C2 (no hot bin) -- so only past that share.  Variant bit 0: never.
+  const bool hotrank = !HS && plan[PLAN_HS] != 0u && !((dbg >> 27) & 1);
+  const uint32_t hb0 = plan[3 * FS + 1], hb1 = plan[3 * FS + 2];  // NOKEY: none
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const uint32_t TB = FS + 2 * ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
           pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
         }
       } else {
-        if ((dbg >> 27) & 1) {
+        if (!hotrank) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
         } else {
@@ -473,7 +476,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
-    if (!HS && !((dbg >> 27) & 1)) {  // (variant bit 0: every bin by LDS atomics)
+    if (hotrank) {
       // ranks: the batch's two hottest bins (k_stplan; e.g. a Zipf head's direct tile,
       // ~1/4 of C3) by wave ballots -- one LDS atomic per wave and bin for all PT
       // slots, and consecutive stage slots for a wave's hot samples -- the other bins
@@ -800,7 +803,7 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       const uint64_t v = ks[h] >> 11;
       plan[3 * FS + 1 + h] = (v > 0 && v * 128 >= grand) ? (uint32_t)(ks[h] & 2047u) : NOKEY;
     }
-    plan[PLAN_HS] = (hot_bins & 2) && grand > 0 && (ks[0] >> 11) * 2 >= grand ? 1u : 0u;
+    plan[PLAN_HS] = grand > 0 && (ks[0] >> 11) * 2 >= grand ? 1u : 0u;  // k_bin1: ballot ranks
     // next batch's k_count hints: the count columns of the two biggest tiles
     // (both halves of a tile that will be split); aggregation only
     uint32_t hkey[4] = {NOKEY, NOKEY, NOKEY, NOKEY};
