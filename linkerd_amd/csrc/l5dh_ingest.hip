@@ -610,9 +610,14 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       const uint32_t v = coltot[cur[SPLIT_LIST + si]];
       if (v >= thr_min && v > 0) atomicAdd(&lhd[31 - __clz((int)v)], 1u);
     }
-  for (uint32_t t = j; t < F; t += 1024) {
-    const uint32_t v = coltot[t];
-    if (v >= split_min && v > 0) atomicAdd(&lhs[31 - __clz((int)v)], 1u);
+  {  // F <= 32768 tiles: a thread's <= 32 totals are loaded at once (one latency, not 32)
+    constexpr int PF = 32;
+    uint32_t tv[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) tv[k] = j + 1024u * k < F ? coltot[j + 1024u * k] : 0u;
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+      if (tv[k] >= split_min && tv[k] > 0) atomicAdd(&lhs[31 - __clz((int)tv[k])], 1u);
   }
   __syncthreads();
   if (j < 2) {

@@ -685,8 +685,10 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   const bool keep = !(final_mode && reset);
   const bool single = tot <= hot_chunk;
   uint32_t* hist = smem;                          // [16][1800]
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] value sums
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + 16 * 64);  // [LUT2_N]
+  // [16][64] lane-private u32 value sums: a lane counts <= hot_chunk / 1024 records
+  // (hot_chunk <= 2^20) of values < 2^21 per item; the region is sized for u64
+  uint32_t* vsl = smem + 16 * HROW;
+  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);  // [LUT2_N]
   uint32_t* wq = reinterpret_cast<uint32_t*>(lut2 + LUT2_N) + w * 256;  // this wave's own-half queue
   {
     uint4* q = reinterpret_cast<uint4*>(smem);
@@ -699,7 +701,7 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   for_half_records(segs, t, vlo, vhi, half, wq, [&](const uint32_t (&rv)[4]) {
     count_batch<4>(
         rv, lut2, [&](uint32_t loc, uint32_t b) { if (!(g_dbg & 0x2000)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-        [&](uint32_t loc, uint32_t v) { if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
+        [&](uint32_t loc, uint32_t v) { if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], v); });
   });
   __syncthreads();
   const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
@@ -746,8 +748,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   uint32_t* hist = smem;                                                              // [16][1800]
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] value sums
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + 16 * 64);                              // [LUT2_N]
+  uint32_t* vsl = smem + 16 * HROW;  // [16][64] lane-private u32 value sums (as in k_accum_hot)
+  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);  // [LUT2_N]
   {
     uint4* q = reinterpret_cast<uint4*>(smem);
     for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
@@ -785,7 +787,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       }
       count_batch<8>(
           x, lut2, [&](uint32_t loc, uint32_t b) { if (!(L5DH_EXP & 2)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-          [&](uint32_t loc, uint32_t v) { if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); });
+          [&](uint32_t loc, uint32_t v) { if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], v); });
     }
   }
   __syncthreads();
