@@ -250,6 +250,45 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds /*
   return r;
 }
 
+// Four independent exclusive scans in one pass (one set of barriers): v[k] per
+// thread -> its exclusive prefix, tot[k] the block totals.  lds: [NT/64 + 1] uint4.
+template <int NT = 1024>
+__device__ __forceinline__ void block_excl_scan4(uint32_t (&v)[4], uint4* lds, uint32_t (&tot)[4]) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  uint32_t x[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t y = __shfl_up(x[k], d, 64);
+      if (lane >= d) x[k] += y;
+    }
+  }
+  if (lane == 63) lds[w] = make_uint4(x[0], x[1], x[2], x[3]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < NW; ++k) {
+      const uint4 q = lds[k];
+      lds[k] = acc;
+      acc = make_uint4(acc.x + q.x, acc.y + q.y, acc.z + q.z, acc.w + q.w);
+    }
+    lds[NW] = acc;
+  }
+  __syncthreads();
+  const uint4 b = lds[w], t = lds[NW];
+  const uint32_t bb[4] = {b.x, b.y, b.z, b.w};
+  const uint32_t tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = bb[k] + x[k] - v[k];
+    tot[k] = tt[k];
+  }
+  __syncthreads();
+}
+
 
 // Bucket of a non-negative key v < Int.MaxValue, bit-identical to
 // upper_bound(limits, v) (== the Arrays.binarySearch insertion rule of

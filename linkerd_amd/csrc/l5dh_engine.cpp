@@ -491,7 +491,9 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
       const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
       HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
                               (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
-                              1,  // the hot k_bin1 bins (ballot ranking when one holds >= half)
+                              // the hot k_bin1 bins (ballot ranking when one holds >= half); all 8
+                              // for the lane-private-slot development variant (L5DH_DBG bit 22)
+                              1 | (((c->dbg >> 22) & 1) ? 4 : 0),
                               c->stream));
       c->split_cur ^= 1;
     }

@@ -202,11 +202,33 @@ __global__ __launch_bounds__(1024) void k_tilescan(uint32_t* __restrict__ coltot
   uint32_t v[PT];
   uint32_t s = 0, tot;
   if (per <= PT) {
-#pragma unroll
-    for (int k = 0; k < PT; ++k) v[k] = ((uint32_t)k < per && t0 + k < F) ? coltot[t0 + k] : 0u;
+    // a thread's <= 32 consecutive tiles span <= 2 split words; every load (totals,
+    // split words, half totals) is issued before any store (the split tiles' sums
+    // are written back to coltot[t] after the loads)
+    const uint32_t wb = t0 >> 5;
+    const uint32_t sw0 = t0 < F ? split[SPLIT_BITS + wb] : 0u, sp0 = t0 < F ? split[SPLIT_PRE + wb] : 0u;
+    const uint32_t sw1 = (wb + 1) * 32 < F ? split[SPLIT_BITS + wb + 1] : 0u;
+    const uint32_t sp1 = (wb + 1) * 32 < F ? split[SPLIT_PRE + wb + 1] : 0u;
+    uint32_t h[PT];
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      if ((uint32_t)k < per && t0 + k < F) v[k] = tile_total(t0 + k, v[k]);
+      const uint32_t t = t0 + k;
+      const bool in = (uint32_t)k < per && t < F;
+      v[k] = in ? coltot[t] : 0u;
+      const bool hi = (t >> 5) != wb;
+      const uint32_t wd = hi ? sw1 : sw0, bit = 1u << (t & 31u);
+      h[k] = 0u;
+      if (in && (wd & bit)) {
+        const uint32_t si = (hi ? sp1 : sp0) + (uint32_t)__popc(wd & (bit - 1u));
+        h[k] = 1u + coltot[F + 2 * si] + coltot[F + 2 * si + 1];  // +1: split (a split tile may be empty)
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      if (h[k]) {
+        v[k] += h[k] - 1u;
+        coltot[t0 + k] = v[k];
+      }
       s += v[k];
     }
     uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
@@ -594,7 +616,7 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
                                                  uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
                                                  uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax,
                                                  uint32_t split_min, int hot_bins) {
-  __shared__ uint32_t lds[17];
+  __shared__ uint4 lds4[17];
   __shared__ unsigned long long best[16];
   __shared__ uint32_t lhd[33], lhs[33];
   __shared__ uint32_t sthr[2];
@@ -699,10 +721,10 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
       gsz = (uint32_t)G;
     }
   }
-  uint32_t total, nnt, ndtot;
-  const uint32_t e = block_excl_scan<1024>(nb, lds, &total);
-  const uint32_t ne = block_excl_scan<1024>(nn, lds, &nnt);
-  const uint32_t de = block_excl_scan<1024>(ndt, lds, &ndtot);
+  uint32_t sv3[4] = {nb, nn, ndt, 0u}, st3[4];
+  block_excl_scan4<1024>(sv3, lds4, st3);
+  const uint32_t e = sv3[0], ne = sv3[1], de = sv3[2];
+  const uint32_t total = st3[0], nnt = st3[1], ndtot = st3[2];
   // this thread's NHOT biggest k_bin1 bins, descending: (records << 11 | bin)
   unsigned long long bk[NHOT] = {};
   auto push = [&](unsigned long long k) {
@@ -788,9 +810,13 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   // (only the lane-private hot-slot variants of k_bin1 use them: 16 barriers saved otherwise)
   unsigned long long ks[NHOT] = {};
   int head = 0;  // this thread's first bin not yet selected
+  // the hottest bins: 2 for the ballot ranking; all NHOT for the lane-private-slot
+  // development variant (hot_bins bit 2) -- each is a block reduction
+  const int nh = (hot_bins & 4) ? NHOT : 2;
   if (hot_bins) {
 #pragma unroll
     for (int q = 0; q < NHOT; ++q) {
+      if (q >= nh) break;
       unsigned long long mine = 0;
 #pragma unroll
       for (int r = 0; r < NHOT; ++r)

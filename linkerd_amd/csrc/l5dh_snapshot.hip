@@ -163,21 +163,25 @@ __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int fina
 
 __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
                                                  uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
-  __shared__ uint32_t lds[4][17];
+  __shared__ uint4 lds4[17];
   __shared__ uint32_t base[4];
   const uint32_t B = gridDim.x;
-  // workgroup bases: exclusive sums of the earlier workgroups' counts (B <= 1024 x 1024 tiles)
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t x = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
-    const uint32_t y = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
-    uint32_t tx = 0, ty = 0;
-    block_excl_scan<1024>(x, lds[k], &tx);
-    if (blockIdx.x == 0) block_excl_scan<1024>(y, lds[k], &ty);
-    if (threadIdx.x == 0) {
-      base[k] = tx;
-      if (blockIdx.x == 0) {  // header: cold items, big tiles, mixed-half items, split items
-        plan.header[k] = ty;
-        plan.header_host[k] = ty;  // read by the host after the stream sync (no copy to enqueue)
+  // workgroup bases: the earlier workgroups' counts (B <= 1024: a thread per workgroup),
+  // summed by one reduction; workgroup 0 also writes the header totals
+  {
+    uint32_t x[4], tx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
+    block_excl_scan4<1024>(x, lds4, tx);
+    if (threadIdx.x < 4) base[threadIdx.x] = tx[threadIdx.x];
+    if (blockIdx.x == 0) {
+      uint32_t y[4], ty[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
+      block_excl_scan4<1024>(y, lds4, ty);
+      if (threadIdx.x < 4) {  // header: cold items, big tiles, mixed-half items, split items
+        plan.header[threadIdx.x] = ty[threadIdx.x];
+        plan.header_host[threadIdx.x] = ty[threadIdx.x];  // read by the host in development builds
       }
     }
   }
@@ -189,10 +193,12 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
     tot = plan.tile_tot[t];
     c = plan_classify(segs, t, tot, final_mode, cold_limit, hot_chunk);
   }
-  uint32_t ca = base[0] + block_excl_scan<1024>(c.ci, lds[0], nullptr);
-  const uint32_t xa = base[1] + block_excl_scan<1024>(c.hot, lds[1], nullptr);
-  uint32_t ha = base[2] + block_excl_scan<1024>(c.hi, lds[2], nullptr);
-  uint32_t sa = base[3] + block_excl_scan<1024>(c.si, lds[3], nullptr);
+  uint32_t pv[4] = {c.ci, c.hot, c.hi, c.si}, ptot[4];
+  block_excl_scan4<1024>(pv, lds4, ptot);
+  uint32_t ca = base[0] + pv[0];
+  const uint32_t xa = base[1] + pv[1];
+  uint32_t ha = base[2] + pv[2];
+  uint32_t sa = base[3] + pv[3];
   if (t >= F) return;
   uint8_t flags = dirty[t] ? TF_DIRTY : 0;
   if (c.hot) {
