@@ -126,6 +126,15 @@ const int32_t* l5dh_limits(size_t* n);
  * occurrence; all valid samples are ingested. */
 int l5dh_ingest(l5dh_ctx* ctx, const uint32_t* series, const float* values, size_t n);
 
+/* The same without waiting for the copy of host buffers: *ticket identifies the
+ * call, and the caller keeps the buffers unchanged until l5dh_ingest_wait(ctx,
+ * ticket) returns (a JNI thread double-buffers its pinned staging this way, so
+ * the PCIe copy of one buffer overlaps the filling of the other).  Tickets grow;
+ * waiting for a ticket also completes every earlier one.  Device buffers follow
+ * l5dh_ingest's rules, with the ticket standing for "consumed". */
+int l5dh_ingest_async(l5dh_ctx* ctx, const uint32_t* series, const float* values, size_t n, uint64_t* ticket);
+int l5dh_ingest_wait(l5dh_ctx* ctx, uint64_t ticket);
+
 /* Reference: Metric.Stat.snapshot() + reset() per Stat as driven by
  * AdminMetricsExportTelemeter.snapshotHistograms (AdminMetricsExportTelemeter.scala:154-162),
  * batched over series [first, first+count).  out (nullable) receives one

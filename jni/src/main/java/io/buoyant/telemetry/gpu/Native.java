@@ -23,6 +23,8 @@ public final class Native {
   public static native int close(long ctx);
   public static native int[] limits();
   public static native int ingest(long ctx, ByteBuffer ids, ByteBuffer values, int n);
+  public static native long ingestAsync(long ctx, ByteBuffer ids, ByteBuffer values, int n);
+  public static native int ingestWait(long ctx, long ticket);
   public static native int snapshot(long ctx, int first, int count, ByteBuffer out, ByteBuffer counts, boolean reset);
   public static native long peek(long ctx, int series, ByteBuffer out, int cap);
   public static native int sync(long ctx);

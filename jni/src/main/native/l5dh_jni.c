@@ -51,6 +51,21 @@ JNIEXPORT jint JNICALL Java_io_buoyant_telemetry_gpu_Native_ingest(JNIEnv* env, 
   return l5dh_ingest(CTX(ctx), (const uint32_t*)ADDR(ids), (const float*)ADDR(values), (size_t)n);
 }
 
+/* long ingestAsync(ctx, ids, values, n): ticket (>= 0) or -errno; the buffers stay
+ * untouched until ingestWait(ctx, ticket) (double-buffered per-thread staging) */
+JNIEXPORT jlong JNICALL Java_io_buoyant_telemetry_gpu_Native_ingestAsync(JNIEnv* env, jclass k, jlong ctx, jobject ids,
+                                                                          jobject values, jint n) {
+  (void)k;
+  uint64_t t = 0;
+  const int rc = l5dh_ingest_async(CTX(ctx), (const uint32_t*)ADDR(ids), (const float*)ADDR(values), (size_t)n, &t);
+  return rc == 0 ? (jlong)t : (jlong)rc;
+}
+
+JNIEXPORT jint JNICALL Java_io_buoyant_telemetry_gpu_Native_ingestWait(JNIEnv* env, jclass k, jlong ctx, jlong ticket) {
+  (void)env; (void)k;
+  return l5dh_ingest_wait(CTX(ctx), (uint64_t)ticket);
+}
+
 /* snapshot(ctx, first, count, out: count*88 B or null, counts: count*1798*4 B or null, reset) */
 JNIEXPORT jint JNICALL Java_io_buoyant_telemetry_gpu_Native_snapshot(JNIEnv* env, jclass k, jlong ctx, jint first,
                                                                       jint count, jobject out, jobject counts,

@@ -15,7 +15,9 @@ import java.util.concurrent.ConcurrentLinkedQueue
  *    MetricsTree.scala:85-93; MetricsTree.prune via MetricsPruningModule.scala:14-39);
  *    a released id is cleared on the GPU before it is reused.
  *  - `add` appends to the calling thread's pinned staging buffers (direct ByteBuffers
- *    over l5dh_pin_alloc memory); a full buffer goes to the GPU in one l5dh_ingest.
+ *    over l5dh_pin_alloc memory), two per thread: a full buffer goes to the GPU with
+ *    l5dh_ingest_async and the thread fills the other one while it is copied (it
+ *    waits for that buffer's ticket before refilling it).
  *  - every read (summary / peek / reset / snapshotAll) flushes all staging buffers
  *    first, then makes ONE engine call, so a reset cannot lose a sample that another
  *    thread flushed in between (Metric.scala:44-51 holds one lock for the same reason).
@@ -50,24 +52,38 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     b.order(ByteOrder.LITTLE_ENDIAN)
   }
 
-  /** One thread's staged Stat.add calls. */
+  /** One thread's staged Stat.add calls: two pinned buffer pairs, double-buffered. */
   private final class Staging {
-    val ids: ByteBuffer = pinned(4L * batch)
-    val values: ByteBuffer = pinned(4L * batch)
-    var n = 0
+    private[this] val ids = Array(pinned(4L * batch), pinned(4L * batch))
+    private[this] val values = Array(pinned(4L * batch), pinned(4L * batch))
+    private[this] val ticket = Array(0L, 0L) // l5dh_ingest_async ticket of each pair (0: free)
+    private[this] var cur = 0
+    private[this] var n = 0
 
     def add(id: Int, value: Float): Unit = synchronized {
-      ids.putInt(4 * n, id)
-      values.putFloat(4 * n, value)
+      ids(cur).putInt(4 * n, id)
+      values(cur).putFloat(4 * n, value)
       n += 1
-      if (n == batch) flushLocked()
+      if (n == batch) flushLocked(waitAll = false)
     }
 
-    def flush(): Unit = synchronized(flushLocked())
+    /** Everything staged reaches the library; returns once both buffers are free. */
+    def flush(): Unit = synchronized(flushLocked(waitAll = true))
 
-    private[this] def flushLocked(): Unit = if (n > 0) {
-      check(Native.ingest(ctx, ids, values, n), "l5dh_ingest")
-      n = 0 // the library has copied the batch when ingest returns
+    private[this] def flushLocked(waitAll: Boolean): Unit = {
+      if (n > 0) {
+        val t = Native.ingestAsync(ctx, ids(cur), values(cur), n)
+        check(t, "l5dh_ingest_async")
+        ticket(cur) = t
+        n = 0
+        cur ^= 1
+        // the other pair is refilled next: its copy must be done
+        if (ticket(cur) != 0) { check(Native.ingestWait(ctx, ticket(cur)), "l5dh_ingest_wait"); ticket(cur) = 0 }
+      }
+      if (waitAll) for (k <- 0 to 1 if ticket(k) != 0) {
+        check(Native.ingestWait(ctx, ticket(k)), "l5dh_ingest_wait")
+        ticket(k) = 0
+      }
     }
   }
 

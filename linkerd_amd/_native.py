@@ -70,6 +70,8 @@ SIGNATURES = {
     "l5dh_close": (_c.c_int, [_vp]),
     "l5dh_limits": (_c.POINTER(_c.c_int32), [_c.POINTER(_c.c_size_t)]),
     "l5dh_ingest": (_c.c_int, [_vp, _vp, _vp, _c.c_size_t]),
+    "l5dh_ingest_async": (_c.c_int, [_vp, _vp, _vp, _c.c_size_t, _c.POINTER(_c.c_uint64)]),
+    "l5dh_ingest_wait": (_c.c_int, [_vp, _c.c_uint64]),
     "l5dh_snapshot": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _vp, _vp, _c.c_int]),
     "l5dh_peek": (_c.c_int, [_vp, _c.c_uint32, _vp, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     "l5dh_export_state": (_c.c_int, [_vp, _c.c_uint32, _c.c_uint32, _vp, _vp, _c.c_int]),

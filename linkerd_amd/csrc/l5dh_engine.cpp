@@ -211,6 +211,12 @@ struct l5dh_ctx {
   size_t ring_fill = 0;
   size_t ring_cap = 0;  // samples (0: every batch is binned at once)
   hipEvent_t ev_copy = nullptr;
+  // asynchronous ingest: ticket t's inputs are consumed when tick_ev[t % NTICK] (recorded
+  // for a ticket >= t, stream order) completes
+  static constexpr int NTICK = 64;
+  hipEvent_t tick_ev[NTICK] = {};
+  uint64_t tick_of[NTICK] = {};
+  uint64_t tick_next = 0, tick_done = 0;
   uint32_t err_reported = 0;  // invalid-id reports already returned (h_header[4] is the device's count)
   // fleet merge (RCCL)
   ncclComm_t comm = nullptr;
@@ -533,12 +539,35 @@ int wait_inputs(l5dh_ctx* c) {
   return 0;
 }
 
-int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n) {
+// Asynchronous ingest: the inputs of ticket t are consumed once its event completes.
+int issue_ticket(l5dh_ctx* c, uint64_t* ticket) {
+  const uint64_t t = ++c->tick_next;
+  const int slot = (int)(t % l5dh_ctx::NTICK);
+  if (!c->tick_ev[slot]) HIPCHK(c, hipEventCreateWithFlags(&c->tick_ev[slot], hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(c->tick_ev[slot], c->stream));
+  c->tick_of[slot] = t;
+  *ticket = t;
+  return 0;
+}
+
+int wait_ticket(l5dh_ctx* c, uint64_t t) {
+  if (t <= c->tick_done) return 0;
+  if (t > c->tick_next) return fail(c, -EINVAL, "unknown ingest ticket");
+  const int slot = (int)(t % l5dh_ctx::NTICK);
+  // the slot holds t or a later ticket (recorded later on the same stream)
+  HIPCHK(c, hipEventSynchronize(c->tick_ev[slot]));
+  c->tick_done = std::max(c->tick_done, c->tick_of[slot]);
+  return 0;
+}
+
+int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n, uint64_t* ticket = nullptr) {
+  if (ticket) *ticket = c->tick_next;  // nothing new to wait for (n == 0)
   if (n == 0) return 0;
   const bool dev = is_device_ptr(series) && is_device_ptr(values);
   // caller-stream contexts are stream ordered for device inputs; otherwise the
-  // call returns once nothing of the caller's memory is still to be read
-  const bool wait = !dev || c->stream == c->own_stream;
+  // call returns once nothing of the caller's memory is still to be read, or, in
+  // the asynchronous form, with a ticket to wait for
+  const bool wait = (!dev || c->stream == c->own_stream) && !ticket;
   if (c->ring_cap && n <= c->ring_cap / 2) {
     int r;
     if (c->ring_fill + n > c->ring_cap && (r = flush_ring(c))) return r;
@@ -552,6 +581,7 @@ int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
                                c->stream));
     }
     c->ring_fill += n;
+    if (ticket) return issue_ticket(c, ticket);
     return wait ? wait_inputs(c) : 0;
   }
   int r = flush_ring(c);
@@ -562,6 +592,7 @@ int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
     const size_t m = std::min(n - o, MAX_BATCH);
     if ((r = do_ingest(c, series + o, values + o, m))) return r;
   }
+  if (ticket) return issue_ticket(c, ticket);
   return wait ? wait_inputs(c) : 0;
 }
 
@@ -833,6 +864,8 @@ int l5dh_close(l5dh_ctx* c) {
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_join) hipEventDestroy(c->ev_join);
   if (c->ev_copy) hipEventDestroy(c->ev_copy);
+  for (hipEvent_t e : c->tick_ev)
+    if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return 0;
@@ -845,6 +878,22 @@ int l5dh_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
   hipSetDevice(c->device);
   const int r = ingest_impl(c, series, values, n);
   return r ? r : check_err(c);
+}
+
+int l5dh_ingest_async(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n, uint64_t* ticket) {
+  if (!c || !ticket) return -EINVAL;
+  if (n && (!series || !values)) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  const int r = ingest_impl(c, series, values, n, ticket);
+  return r ? r : check_err(c);
+}
+
+int l5dh_ingest_wait(l5dh_ctx* c, uint64_t ticket) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  return wait_ticket(c, ticket);
 }
 
 int l5dh_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, int32_t* counts_out, int reset) {

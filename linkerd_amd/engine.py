@@ -135,6 +135,24 @@ class HistogramEngine:
         vp = self._buf(values, (np.float32,), "values")
         self._check(self._lib.l5dh_ingest(self._ctx, sp, vp, n), "l5dh_ingest")
 
+    def ingest_async(self, series, values) -> int:
+        """l5dh_ingest_async: returns a ticket; the buffers must stay unchanged until
+        ingest_wait(ticket) (host numpy buffers must stay referenced by the caller)."""
+        for name, x, dts in (("series", series, (np.uint32, np.int32)), ("values", values, (np.float32,))):
+            if isinstance(x, np.ndarray) and (x.dtype.type not in dts or not x.flags["C_CONTIGUOUS"]):
+                raise TypeError(f"ingest_async: {name} must be C-contiguous {dts[0].__name__} (no conversion copy)")
+        n = _numel(series)
+        if n != _numel(values):
+            raise ValueError("series and values differ in length")
+        sp = self._buf(series, (np.uint32, np.int32), "series")
+        vp = self._buf(values, (np.float32,), "values")
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.l5dh_ingest_async(self._ctx, sp, vp, n, ctypes.byref(t)), "l5dh_ingest_async")
+        return t.value
+
+    def ingest_wait(self, ticket: int) -> None:
+        self._check(self._lib.l5dh_ingest_wait(self._ctx, int(ticket)), "l5dh_ingest_wait")
+
     def snapshot(self, first: int = 0, count: Optional[int] = None, reset: bool = True,
                  with_counts: bool = False):
         """Summaries (numpy structured, HistogramSummary field order) and optional

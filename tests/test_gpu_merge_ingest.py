@@ -113,6 +113,49 @@ def test_streaming_small_batches_from_pinned_memory(oracle, piece):
     eng.close()
 
 
+@pytest.mark.parametrize("piece,stage", [(65536, None), (777, None), (1 << 20, 0)], ids=["64k", "777", "1m-unstaged"])
+def test_async_double_buffered_ingest(oracle, piece, stage):
+    """l5dh_ingest_async with two pinned staging pairs (the JNI thread's shape): a pair
+    is refilled only after its ticket completed, and overwritten right after."""
+    from linkerd_amd.engine import HistogramEngine
+    S, n = 20_000, 3_000_000
+    series, vals = synth.c3(S=S, N=n, seed=72)
+    lib = N.load()
+    eng = HistogramEngine(S)
+    if stage is not None:
+        eng.set_param(N.PARAM_STAGE_SAMPLES, stage)
+    bufs = [(_pinned(lib, piece, np.uint32), _pinned(lib, piece, np.float32)) for _ in range(2)]
+    tickets = [0, 0]
+    import ctypes as C
+    t = C.c_uint64(0)
+    for i, off in enumerate(range(0, n, piece)):
+        k = i & 1
+        if tickets[k]:
+            eng.ingest_wait(tickets[k])
+        (ps, hs), (pv, hv) = bufs[k]
+        hs[:] = 0xFFFFFFFF
+        hv[:] = np.nan
+        m = min(piece, n - off)
+        hs[:m] = series[off:off + m]
+        hv[:m] = vals[off:off + m]
+        eng._check(lib.l5dh_ingest_async(eng._ctx, ps, pv, m, C.byref(t)), "l5dh_ingest_async")
+        assert t.value > max(tickets)
+        tickets[k] = t.value
+    eng.ingest_wait(max(tickets))
+    for (ps, hs), (pv, hv) in bufs:  # everything consumed: the buffers may go
+        hs[:] = 0xFFFFFFFF
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    eng.sync()
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals, threads=8)
+    np.testing.assert_array_equal(counts, o.counts())
+    _eq_summaries(got, o.snapshot())
+    for (ps, _), (pv, _) in bufs:
+        lib.l5dh_pin_free(ps)
+        lib.l5dh_pin_free(pv)
+    eng.close()
+
+
 def test_staged_device_batches_and_deferred_errors(oracle):
     import torch
     from linkerd_amd.engine import HistogramEngine
