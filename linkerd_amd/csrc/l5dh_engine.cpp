@@ -316,6 +316,19 @@ bool is_device_ptr(const void* p) {
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Device-visible address of page-locked host memory (hipHostMalloc / registered),
+// or nullptr for device or pageable memory.
+const void* host_mapped_ptr(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  return static_cast<const char*>(a.devicePointer) + (static_cast<const char*>(p) - static_cast<const char*>(a.hostPointer));
+}
+
 int ensure(l5dh_ctx* c, DevBuf& b, size_t bytes) {
   if (b.cap >= bytes) return 0;
   if (b.p) {
@@ -575,10 +588,18 @@ int ingest_impl(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
       return r;
     {
       KTimer kt(c, L5DH_K_COPY);
-      HIPCHK(c, hipMemcpyAsync(static_cast<uint32_t*>(c->ring_series.p) + c->ring_fill, series, n * 4, hipMemcpyDefault,
-                               c->stream));
-      HIPCHK(c, hipMemcpyAsync(static_cast<float*>(c->ring_values.p) + c->ring_fill, values, n * 4, hipMemcpyDefault,
-                               c->stream));
+      uint32_t* rs = static_cast<uint32_t*>(c->ring_series.p) + c->ring_fill;
+      float* rv = static_cast<float*>(c->ring_values.p) + c->ring_fill;
+      // pinned host batches: one zero-copy kernel (variant bit 1: DMA copies instead)
+      const void* hs = dev || (c->variant & 2) ? nullptr : host_mapped_ptr(series);
+      const void* hv = hs ? host_mapped_ptr(values) : nullptr;
+      if (hs && hv) {
+        HIPCHK(c, launch_fetch_host(static_cast<const uint32_t*>(hs), static_cast<const uint32_t*>(hv), rs,
+                                    reinterpret_cast<uint32_t*>(rv), n, c->stream));
+      } else {
+        HIPCHK(c, hipMemcpyAsync(rs, series, n * 4, hipMemcpyDefault, c->stream));
+        HIPCHK(c, hipMemcpyAsync(rv, values, n * 4, hipMemcpyDefault, c->stream));
+      }
     }
     c->ring_fill += n;
     if (ticket) return issue_ticket(c, ticket);

@@ -1013,7 +1013,28 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   }
 }
 
+// Small host batches into the staging ring: the GPU reads pinned host memory
+// directly (zero-copy over PCIe) -- one kernel for both arrays, instead of two
+// DMA copies whose setup dominates at 64K samples (35 us per pair measured).
+__global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__ hs, const uint32_t* __restrict__ hv,
+                                                    uint32_t* __restrict__ ds, uint32_t* __restrict__ dv, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t s = hs[i], v = hv[i];
+    ds[i] = s;
+    dv[i] = v;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
+                             hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_fetch_host, dim3((unsigned)blocks), dim3(256), 0, st, hs, hv, ds, dv, n);
+  return hipGetLastError();
+}
 
 // ------------------------------------------------------------------------
 hipError_t set_ingest_attributes() {

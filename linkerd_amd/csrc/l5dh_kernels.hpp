@@ -173,6 +173,9 @@ hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb
 // dense rows ext[count][1798] + ext_total[count].
 hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out,
                        int reset, int64_t* totals_out, hipStream_t st);
+// Copy n (series, value) pairs from device-visible pinned host memory (zero-copy).
+hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
+                             hipStream_t st);
 hipError_t set_ingest_attributes();
 hipError_t set_snapshot_attributes();
 hipError_t set_snapshot_debug(int dbg);
