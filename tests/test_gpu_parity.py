@@ -188,6 +188,27 @@ def test_split_tiles_across_batches(oracle, direct_max):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"split {it}")
 
 
+def test_split_bins_one_bucket(oracle):
+    """A split half-tile whose 300k records per batch all fall in ONE bucket: one LDS
+    bin of a 2^18-record split item reaches 2^18 (u32 bins), the dense state row
+    accumulates across batches."""
+    rng = np.random.default_rng(5)
+    S = 64
+    eng = _engine(S, 2)
+    eng.set_param(N.PARAM_SPLIT_MIN, 1000)
+    o = oracle.OracleHistograms(S)
+    for it in range(3):  # the first batch makes tile 0 split for the later ones
+        series = np.concatenate([np.zeros(300_000, np.uint32), rng.integers(0, S, 20_000).astype(np.uint32)])
+        vals = np.concatenate([np.full(300_000, 5.0, np.float32),
+                               np.exp(2 + rng.standard_normal(20_000)).astype(np.float32)])
+        perm = rng.permutation(series.size)
+        eng.ingest(series[perm], vals[perm])
+        o.ingest(series[perm], vals[perm])
+        got, counts = eng.snapshot(reset=it == 1, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"batch {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=it == 1), f"capacity {it}")
+
+
 def test_range_snapshot_peek_export(oracle):
     rng = np.random.default_rng(21)
     S = 500
