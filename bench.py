@@ -61,12 +61,12 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # (COST_PS_PER_SAMPLE per Zipf-expected sample + COST_PS_PER_SERIES per series row)
 # times a measured correction per Zipf-rank range -- each range's measured shard
 # time over its base-model time, from the 8 single-GPU runs of `--shard r/8`
-# (profiles/r02c_shards.jsonl, less 0.045 ms of per-step overhead): direct
+# (the sweep before profiles/r02f_shards.jsonl, which is this calibration's result): direct
 # tiles, split tiles through level 2 and cold tiles cost differently per sample
 COST_PS_PER_SAMPLE = 6.5
 COST_PS_PER_SERIES = 1700.0
-COST_CALIBRATION = ((0, 1.115), (5, 1.005), (60, 1.025), (916, 1.115), (8844, 1.205), (53451, 1.185),
-                    (235685, 1.155), (567404, 1.175))  # (first Zipf rank, ms of that r/8 shard)
+COST_CALIBRATION = ((0, 0.9636), (5, 1.2207), (84, 1.1982), (1446, 1.1614), (12689, 1.2163), (66634, 1.1499),
+                    (255661, 1.1597), (585238, 1.1694))  # (first Zipf rank, ms of that r/8 shard)
 
 
 def parse():
