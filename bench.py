@@ -76,6 +76,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=["c3", "c2", "c1", "c4"], default="c3")
     p.add_argument("--rotate", type=int, default=3, help="distinct batches (seeds) cycled over the steps")
+    p.add_argument("--hot-shift", action="store_true",
+                   help="c3/c4: batch k's series ids rotated by k/rotate of the range, so the hot set moves every step")
     p.add_argument("--piece", type=int, default=0, help="stream from pinned host memory in calls of this many samples")
     p.add_argument("--shard", default=None, help="r/W: run rank r's C3 shard of a W-way split on this one GPU")
     p.add_argument("--series", type=int, default=None, help="series (default: workload's)")
@@ -275,7 +277,18 @@ def load_pmc_traffic(path, pl):
 
 
 # ---------------------------------------------------------------- main
+def result_stream():
+    """The result line's stream: a duplicate of stdout, while fd 1 itself is pointed at
+    stderr, so that library banners (RCCL prints its version block on stdout when a
+    communicator is created) never mix with the ONE JSON line."""
+    out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+    return out
+
+
 def run(args):
+    result_out = result_stream()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -292,7 +305,7 @@ def run(args):
         else:
             plans = [pl]
         if rank == 0:
-            print(json.dumps({"dry_run": True, "world": world, "plans": plans}), flush=True)
+            print(json.dumps({"dry_run": True, "world": world, "plans": plans}), file=result_out, flush=True)
         if distributed:
             dist.destroy_process_group()
         return
@@ -319,6 +332,14 @@ def run(args):
     streaming = args.piece > 0
     R = 1 if streaming else max(1, args.rotate)
     batches = [gen_batch(torch, synth_lib, pl, k, stream) for k in range(R)]
+    if args.hot_shift and pl["workload"] in ("c3", "c4"):
+        # a moving hot set: the split / direct tiles chosen from the previous batch are
+        # the wrong ones (untimed: ids rotated within the rank's range before the run)
+        f, c = pl["first"], pl["count"]
+        for k, (sr, _) in enumerate(batches):
+            if k:
+                sr.copy_(((sr.long() - f + k * c // R) % c + f).to(torch.int32))
+        torch.cuda.synchronize()
     S = pl["count"]
     n = pl["samples"]
 
@@ -476,6 +497,7 @@ def run(args):
                           "ranks, RCCL reduce-scatter of dense counts, summaries of each rank's slice"}
         cfg = {"workload": wl_names[pl["workload"]], "series_total": pl["S_total"], "samples_per_step": total_samples,
                "series_per_gpu": S, "samples_per_gpu_per_step": n, "rotating_batches": R,
+               **({"hot_shift": True} if args.hot_shift else {}),
                "parallelism": (f"sample-sharded x{world}" if fleet else
                                f"series-sharded x{world} (weighted ranges)" if pl["workload"] == "c3" else
                                f"replicas x{world}"),
@@ -497,7 +519,7 @@ def run(args):
         }
         if merge:
             line["merge"] = merge
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if host:
         host[0].l5dh_pin_free(ctypes.c_void_p(host[1]))
         host[0].l5dh_pin_free(ctypes.c_void_p(host[2]))

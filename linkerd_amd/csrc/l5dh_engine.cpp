@@ -1077,7 +1077,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->cold_limit = (uint32_t)v;
       return 0;
     case L5DH_PARAM_HOT_CHUNK:
-      // <= 2^20: a lane of the big-tile kernels sums <= hot_chunk / 1024 values < 2^21 in u32
+      // <= 2^20: an item's records index LDS bins in u32 (and stay far below 2^32)
       if (v < 1024 || v > (1ll << 20)) return fail(c, -EINVAL, "hot chunk must be in [1024, 2^20]");
       c->hot_chunk = (uint32_t)v;
       return 0;

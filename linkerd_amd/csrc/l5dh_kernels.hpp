@@ -36,7 +36,7 @@ constexpr size_t acc_cold_lds(int nser) { return (size_t)nser * CROW * 4 + nser 
 constexpr size_t acc_cold_p_lds(int nser) { return acc_cold_lds(nser) + ROW * 4; }  // + bucket midpoints
 // hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
-constexpr size_t ACC_HOT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8 + 16 * 256 * 4;
+constexpr size_t ACC_HOT_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 8 + 1024 * 8;  // u16 bins of 32 series, u64 sums
 
 constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
 constexpr int LUT2_N = 1024;        // exact bucket + offset LUT for keys < 2^21 (64 direct + 15 octaves x 64)
@@ -84,7 +84,6 @@ struct State {
   uint32_t S, F;
 };
 
-constexpr uint8_t TF_SINGLE = 1;   // big tile finished in place by k_accum_hot (one chunk)
 constexpr uint8_t TF_SPLIT = 2;    // big tile accumulated per half (split in every pending segment)
 constexpr uint8_t TF_DIRTY = 4;    // the tile held live counts when k_plan ran
 

@@ -85,7 +85,6 @@ __global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_
         const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
         for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
         ha += nc;
-        if (tot <= hot_chunk) flags |= TF_SINGLE;
       }
       plan.hot_list[xa++] = t;
     } else if (final_mode || tot > 0) {
@@ -210,7 +209,6 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
       }
     } else {
       for (uint32_t q = 0; q < c.hi; ++q) plan.hot_item[ha + q] = t | (q << 15);
-      if (tot <= hot_chunk) flags |= TF_SINGLE;
     }
     plan.hot_list[xa] = t;
   } else if (c.ci) {
@@ -226,7 +224,7 @@ __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t 
   const uint32_t nh = plan.header[1];
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const uint32_t t = plan.hot_list[i];
-    if (st.dirty[t] || (plan.tile_flags[t] & TF_SINGLE)) continue;  // single-chunk tiles emit in place
+    if (st.dirty[t]) continue;
     const uint32_t s0 = t * TILE;
     const uint32_t s1 = min(st.S, s0 + TILE);
     uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
@@ -343,63 +341,6 @@ __device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, u
       for_records<NT>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), fn);
     }
     vbase += len;
-  }
-}
-
-// Records of tile t in the virtual range [vlo, vhi) whose series lies in half
-// `half` (bit 25 = series-in-tile >> 4), visited by full waves: every lane loads
-// 8 records per block (the next block already in flight: 32 B per lane), the
-// wave compacts its own-half ones, 4 at a time, into its LDS queue (ballot +
-// mbcnt) and hands the queue to fn as one batch of 4 entries per lane (~0u: none).
-template <class Fn>
-__device__ __forceinline__ void for_half_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi,
-                                                 uint32_t half, uint32_t* __restrict__ q, Fn&& fn) {
-  const int lane = lane_id();
-  uint64_t vbase = 0;
-  for (int j = 0; j < segs.n; ++j) {
-    const uint32_t a0 = segs.tbase[j][t];
-    const uint32_t e0 = segs.tbase[j][t + 1];
-    const uint64_t len = e0 - a0;
-    const uint64_t lo = vlo > vbase ? vlo : vbase;
-    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
-    const uint64_t skip = lo - vbase;
-    vbase += len;
-    if (lo >= hi) continue;
-    const uint32_t a = a0 + (uint32_t)skip;
-    const uint32_t e = a + (uint32_t)(hi - lo);
-    const uint32_t* __restrict__ r = segs.recs[j];
-    const uint32_t a4 = a & ~3u;  // 16-B aligned groups; entries outside [a, e) are masked
-    auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
-    uint32_t g = a4 + 4u * threadIdx.x;
-    uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
-    for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
-      const uint4 x0 = n0, x1 = n1;
-      n0 = ld(g + 8u * WG);
-      n1 = ld(g + 12u * WG);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint4 xx = h ? x1 : x0;
-        const uint32_t gh = g + h * 4u * WG;
-        const uint32_t x[4] = {xx.x, xx.y, xx.z, xx.w};
-        uint32_t nq = 0;
-        if (g_dbg & 0x800) {  // timing: loads only
-          if ((x[0] ^ x[1] ^ x[2] ^ x[3]) == 0x12345u) q[lane] = x[0];
-          continue;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool own = gh + k >= a && gh + k < e && ((x[k] >> 25) & 1u) == half;
-          const unsigned long long m = __ballot(own);
-          if (own) q[nq + mask_below(m)] = x[k];
-          nq += (uint32_t)__popcll(m);
-        }
-        if (g_dbg & 0x400) continue;  // timing: no counting
-        uint32_t rv[4];  // nq <= 256: at most 4 entries per lane, handed over as one batch
-#pragma unroll
-        for (int k = 0; k < 4; ++k) rv[k] = lane + 64u * k < nq ? q[lane + 64 * k] : 0xFFFFFFFFu;
-        fn(rv);
-      }
-    }
   }
 }
 
@@ -663,79 +604,90 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
   }
 }
 
-// Big tiles (> cold_limit records): item = (chunk of <= hot_chunk records, half of
-// the tile's series).  Both halves of a chunk are blocks b and b+8 -- the same XCD
-// under the round-robin dispatch (MI355X_MICROARCH.md), so they stream the chunk
-// together and the second read is served by that XCD's L2 (speed only; results
-// never depend on placement).  A tile with one chunk is finished in place (each
-// half owns its 16 series); chunks of bigger tiles flush with global atomics and
-// k_hot_finish completes them.
-__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                  uint32_t cold_limit, uint32_t hot_chunk, int final_mode,
-                                                  int reset) {
-  (void)cold_limit;
+// Big tiles (> cold_limit records) not split in every pending segment: item = (tile,
+// chunk of <= hot_chunk records of its concatenated segments), the whole tile's 32
+// series in u16-packed LDS bins (115 KB, like a cold tile), each record read once.
+// A bin that reaches 2^15 hands 2^15 to the state row (one global atomic; the half
+// never reaches 2^16, so it cannot carry into its neighbour); at the end every
+// nonzero bin is flushed with global atomics into the rows k_hot_init cleared, and
+// k_hot_finish summarizes them.  Lane-private u64 value sums.
+__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  // persistent: virtual blocks vb = blockIdx.x + r * gridDim.x (gridDim.x a multiple of
-  // 16, so both halves of a chunk item stay 8 blocks apart); p grows with r
-  for (uint32_t vb = blockIdx.x;; vb += gridDim.x) {
-  const uint32_t p = (vb / 16) * 8 + (vb % 8);  // chunk item
-  const uint32_t half = (vb / 8) & 1u;
-  if (p >= plan.header[2]) return;
-  const uint32_t hx = plan.hot_item[p];
-  const uint32_t t = hx & 0x7FFFu;
-  const uint32_t sub = hx >> 15;
-  const uint32_t tot = plan.tile_tot[t];
-  (void)hot_chunk;
+  uint32_t* hist = smem;                                                                // [32][CROW] u16 pairs
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + TILE * CROW);  // [32][64]
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);                              // [LUT2_N]
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
-  const bool keep = !(final_mode && reset);
-  const bool single = tot <= hot_chunk;
-  uint32_t* hist = smem;                          // [16][1800]
-  // [16][64] lane-private u32 value sums: a lane counts <= hot_chunk / 1024 records
-  // (hot_chunk <= 2^20) of values < 2^21 per item; the region is sized for u64
-  uint32_t* vsl = smem + 16 * HROW;
-  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);  // [LUT2_N]
-  uint32_t* wq = reinterpret_cast<uint32_t*>(lut2 + LUT2_N) + w * 256;  // this wave's own-half queue
-  {
-    uint4* q = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
-  }
-  __syncthreads();
-  const uint64_t vlo = (uint64_t)sub * hot_chunk;
-  const uint64_t vhi = vlo + hot_chunk < tot ? vlo + hot_chunk : tot;
-  for_half_records(segs, t, vlo, vhi, half, wq, [&](const uint32_t (&rv)[4]) {
-    count_batch<4>(
-        rv, lut2, [&](uint32_t loc, uint32_t b) { if (!(g_dbg & 0x2000)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-        [&](uint32_t loc, uint32_t v) { if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], v); });
-  });
-  __syncthreads();
-  const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
-  const uint32_t s = t * TILE + 16 * half + w;
-  if (s < st.S) {
-    if (single) {
-      const int64_t fix = st.sumfix[s];
-      if (lane == 0 && fix) st.sumfix[s] = 0;
-      emit_series(SrcLds32{hist + w * HROW}, s, my_vsum, fix, st.dirty[t] != 0, keep, final_mode, st, tb, out);
-    } else {
-      uint32_t* grow = st.counts + (size_t)s * ROW;
-      const uint32_t* hrow = hist + w * HROW;
+  const uint32_t nitems = plan.header[2];  // persistent: items blockIdx.x, + gridDim.x, ...
+  for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
+  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    {
+      uint4* q = reinterpret_cast<uint4*>(smem);
+      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const uint32_t hx = plan.hot_item[item];
+    const uint32_t t = hx & 0x7FFFu;
+    const uint64_t vlo = (uint64_t)(hx >> 15) * hot_chunk, vhi = vlo + hot_chunk;
+    uint32_t* tile_rows = st.counts + (size_t)t * TILE * ROW;
+    auto hist_add = [&](uint32_t loc, uint32_t b) {
+      if (g_dbg & 0x2000) return;
+      const uint32_t sh = (b & 1u) * 16u;
+      uint32_t* wd = &hist[(loc & 31u) * CROW + (b >> 1)];
+      const uint32_t old = atomicAdd(wd, 1u << sh);
+      if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add made it 2^15: hand 2^15 over
+        atomicSub(wd, 0x8000u << sh);
+        atomicAdd(&tile_rows[(size_t)(loc & 31u) * ROW + b], 0x8000u);
+      }
+    };
+    auto sum_add = [&](uint32_t loc, uint32_t v) {
+      if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 31u) * 64 + lane], (unsigned long long)v);
+    };
+    uint64_t vbase = 0;
+    for (int j = 0; j < segs.n; ++j) {
+      const uint32_t ta = segs.tbase[j][t], te = segs.tbase[j][t + 1];
+      const uint64_t len = te - ta;
+      const uint64_t lo = vlo > vbase ? vlo : vbase;
+      const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+      const uint64_t skip = lo - vbase;
+      vbase += len;
+      if (lo >= hi) continue;
+      const uint32_t a = ta + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
+      const uint32_t* __restrict__ r = segs.recs[j];
+      auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
+      const uint32_t a4 = a & ~3u;
+      uint32_t g = a4 + 4u * threadIdx.x;
+      uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
+      for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
+        const uint4 x0 = n0, x1 = n1;
+        n0 = ld(g + 8u * WG);
+        n1 = ld(g + 12u * WG);
+        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+        }
+        count_batch<8>(x, lut2, hist_add, sum_add);
+      }
+    }
+    __syncthreads();
+    for (int loc = w; loc < TILE; loc += WG / 64) {
+      const uint32_t s = t * TILE + loc;
+      if (s >= st.S) continue;
+      const uint64_t vsum = wave_sum(vsl[loc * 64 + lane]);
+      uint32_t* grow = tile_rows + (size_t)loc * ROW;
+      const uint32_t* hrow = hist + loc * CROW;
       for (int b0 = 0; b0 < ((g_dbg & 0x1000) ? 0 : NB); b0 += 64) {  // 64 consecutive bins per wave atomic
         const int b = b0 + lane;
-        const uint32_t v = b < NB ? hrow[b] : 0u;
+        const uint32_t v = b < NB ? (hrow[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu : 0u;
         if (__ballot(v != 0u)) {
           if (v) atomicAdd(&grow[b], v);
         }
       }
-      if (lane == 0) {
-        const uint64_t add = my_vsum;
-        if (add) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)add);
-      }
+      if (lane == 0 && vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)vsum);
     }
-  }
-  // dirty[t] of a single-chunk tile is updated by k_hot_finish: the other half may
-  // not have read it yet.
-  __syncthreads();  // the LDS rows are read: the next item may clear them
+    __syncthreads();  // the LDS rows are read: the next item may clear them
   }
 }
 
@@ -754,7 +706,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   uint32_t* hist = smem;                                                              // [16][1800]
-  uint32_t* vsl = smem + 16 * HROW;  // [16][64] lane-private u32 value sums (as in k_accum_hot)
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] u64, as in k_accum_hot
   uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);  // [LUT2_N]
   {
     uint4* q = reinterpret_cast<uint4*>(smem);
@@ -793,7 +745,9 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       }
       count_batch<8>(
           x, lut2, [&](uint32_t loc, uint32_t b) { if (!(L5DH_EXP & 2)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-          [&](uint32_t loc, uint32_t v) { if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], v); });
+          [&](uint32_t loc, uint32_t v) {
+            if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v);
+          });
     }
   }
   __syncthreads();
@@ -823,10 +777,6 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
   for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   const uint32_t t = plan.hot_list[vb >> 1];
   const uint32_t half = vb & 1u;
-  if (plan.tile_flags[t] & TF_SINGLE) {  // emitted by k_accum_hot
-    if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
-    continue;
-  }
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const uint32_t s = t * TILE + 16 * half + w;
@@ -986,10 +936,9 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (max_hot_items) {  // persistent: (chunk, half) pairs 8 blocks apart, a multiple of 16 blocks
-    const uint32_t blocks = ((std::min<uint32_t>(2 * max_hot_items, 2 * ncu) + 15) / 16) * 16;
-    hipLaunchKernelGGL(k_accum_hot, dim3(blocks), dim3(WG), ACC_HOT_LDS, st, segs, plan, state, tb, out, cold_limit,
-                       hot_chunk, final_mode, reset);
+  if (max_hot_items) {  // persistent: one workgroup per CU walking the chunk items
+    hipLaunchKernelGGL(k_accum_hot, dim3(std::min<uint32_t>(max_hot_items, ncu)), dim3(WG), ACC_HOT_LDS, st, segs,
+                       plan, state, tb, hot_chunk);
     return hipGetLastError();
   }
   return hipSuccess;

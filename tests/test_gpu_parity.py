@@ -188,10 +188,12 @@ def test_split_tiles_across_batches(oracle, direct_max):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"split {it}")
 
 
-def test_split_bins_one_bucket(oracle):
+@pytest.mark.parametrize("value", [5.0, 2_000_000.0])
+def test_split_bins_one_bucket(oracle, value):
     """A split half-tile whose 300k records per batch all fall in ONE bucket: one LDS
     bin of a 2^18-record split item reaches 2^18 (u32 bins), the dense state row
-    accumulates across batches."""
+    accumulates across batches.  At 2e6 (the largest payloads below the escape) one
+    lane's value-sum slot of an item takes 4096 x 2e6 > 2^32 (u64 slots)."""
     rng = np.random.default_rng(5)
     S = 64
     eng = _engine(S, 2)
@@ -199,7 +201,7 @@ def test_split_bins_one_bucket(oracle):
     o = oracle.OracleHistograms(S)
     for it in range(3):  # the first batch makes tile 0 split for the later ones
         series = np.concatenate([np.zeros(300_000, np.uint32), rng.integers(0, S, 20_000).astype(np.uint32)])
-        vals = np.concatenate([np.full(300_000, 5.0, np.float32),
+        vals = np.concatenate([np.full(300_000, value, np.float32),
                                np.exp(2 + rng.standard_normal(20_000)).astype(np.float32)])
         perm = rng.permutation(series.size)
         eng.ingest(series[perm], vals[perm])
@@ -207,6 +209,27 @@ def test_split_bins_one_bucket(oracle):
         got, counts = eng.snapshot(reset=it == 1, with_counts=True)
         np.testing.assert_array_equal(counts, o.counts(), err_msg=f"batch {it}")
         _assert_summaries_equal(got, o.snapshot(reset=it == 1), f"capacity {it}")
+
+
+def test_big_tile_bins_past_u16(oracle):
+    """Big tiles outside the split set (k_accum_hot: whole-tile u16 bins): one bin of
+    a 2^18-record item passes 2^15 many times and hands each 2^15 to the state row;
+    a clean and a dirty tile, and a hot set that moves between batches."""
+    rng = np.random.default_rng(17)
+    S = 100
+    eng = _engine(S, 2)
+    o = oracle.OracleHistograms(S)
+    plan = [(0, 7.0, 300_000, False), (40, 1_000_000.0, 200_000, False), (0, 113.0, 70_000, True),
+            (70, 2_000_000.0, 280_000, True)]
+    for it, (sid, value, n, reset) in enumerate(plan):
+        series = np.concatenate([np.full(n, sid, np.uint32), rng.integers(0, S, 20_000).astype(np.uint32)])
+        vals = np.concatenate([np.full(n, value, np.float32), np.exp(2 + rng.standard_normal(20_000)).astype(np.float32)])
+        perm = rng.permutation(series.size)
+        eng.ingest(series[perm], vals[perm])
+        o.ingest(series[perm], vals[perm])
+        got, counts = eng.snapshot(reset=reset, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"batch {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=reset), f"big tile {it}")
 
 
 def test_range_snapshot_peek_export(oracle):
