@@ -28,13 +28,13 @@ constexpr int MAX_SEG = 8;
 constexpr int WG = 1024;            // threads per workgroup of the heavy kernels
 constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow below this
 
-// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold) or 16 u32 rows
-// (hot), lane-private offset sums, the bucket LUT
+// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold, big tiles) or 16 u32
+// rows (split half-tiles), lane-private value sums, the bucket LUT
 constexpr size_t ACC_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 4 + 1024 * 8 + TILE * 8 + 16;
 // cold item of nser series (a tile, or half of one): u16-packed rows, lane-private sums, the LUT, sumfix
 constexpr size_t acc_cold_lds(int nser) { return (size_t)nser * CROW * 4 + nser * 64 * 4 + 1024 * 8 + nser * 8 + 16; }
 constexpr size_t acc_cold_p_lds(int nser) { return acc_cold_lds(nser) + ROW * 4; }  // + bucket midpoints
-// hot: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT, 16 wave queues of 256 records
+// split half-tile: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
 constexpr size_t ACC_HOT_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 8 + 1024 * 8;  // u16 bins of 32 series, u64 sums
 
