@@ -60,7 +60,12 @@ class SeriesRouter:
         self.starts = np.array([s.first for s in self.shards] + [self.shards[-1].first + self.shards[-1].count],
                                dtype=np.int64)
 
-    def route(self, series: np.ndarray, values: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
+    def route(self, series, values) -> List[Tuple]:
+        """Per rank: (local ids, values).  numpy in, numpy out; torch tensors (device or
+        host) in, tensors of the same device out -- a batch resident in HBM is routed
+        in HBM (one stable sort by owner, one host read of the W counts)."""
+        if not isinstance(series, np.ndarray) and hasattr(series, "device"):
+            return self._route_torch(series, values)
         series = np.asarray(series, dtype=np.int64)
         owner = np.searchsorted(self.starts, series, side="right") - 1
         out = []
@@ -68,6 +73,19 @@ class SeriesRouter:
             m = owner == sh.rank
             out.append(((series[m] - sh.first).astype(np.uint32), np.asarray(values)[m].astype(np.float32)))
         return out
+
+    def _route_torch(self, series, values):
+        import torch
+        s = series.to(torch.int64)
+        if series.dtype == torch.int32:  # uint32 ids arrive as int32 bit patterns
+            s = s & 0xFFFFFFFF
+        starts = torch.as_tensor(self.starts, dtype=torch.int64, device=series.device)
+        owner = torch.searchsorted(starts, s, right=True) - 1  # ids past the last shard: owner W
+        order = torch.sort(owner, stable=True).indices
+        counts = torch.bincount(owner.clamp(0, len(self.shards)), minlength=len(self.shards) + 1)
+        parts_s = torch.split(s[order], counts.tolist())
+        parts_v = torch.split(values.to(torch.float32)[order], counts.tolist())
+        return [((parts_s[r] - sh.first).to(torch.int32), parts_v[r]) for r, sh in enumerate(self.shards)]
 
 
 def padded_rows(S: int, world: int) -> int:

@@ -88,6 +88,21 @@ def test_shard_ranges_balanced_and_router():
     assert parts[2][0].tolist() == [3, 0] and parts[2][1].tolist() == [2.0, 5.0]
 
 
+def test_router_torch_tensors_match_numpy():
+    """The tensor path (batches resident in HBM are routed there) gives the numpy
+    path's parts, in the same order, including ids stored as int32 bit patterns."""
+    import torch
+    rng = np.random.default_rng(3)
+    S = 5000
+    shards = fleet.shard_ranges(S, 4, weights=1.0 / (np.arange(S) + 1.0))
+    series = rng.integers(0, S, 20_000).astype(np.uint32)
+    vals = rng.random(20_000).astype(np.float32)
+    want = fleet.SeriesRouter(shards).route(series, vals)
+    got = fleet.SeriesRouter(shards).route(torch.from_numpy(series.view(np.int32)), torch.from_numpy(vals))
+    for (ws, wv), (gs, gv) in zip(want, got):
+        assert np.array_equal(gs.numpy().view(np.uint32), ws) and np.array_equal(gv.numpy(), wv)
+
+
 def _sharded_worker(rank, world, port, S, N, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
