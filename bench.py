@@ -310,13 +310,21 @@ def run(args):
             dist.destroy_process_group()
         return
 
+    # L5DH_BENCH_BACKEND=gloo: the rank harness over gloo with ranks sharing the GPUs
+    # there are (a 1-GPU rehearsal of the multi-rank C3 path; the driver's runs use RCCL)
+    backend = os.environ.get("L5DH_BENCH_BACKEND", "nccl")
     if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gpu = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")  # where reductions run
     # one non-default stream for the generator, torch and the engine (l5dh_set_stream):
     # device inputs and outputs are then stream ordered, no host wait per ingest
     torch.cuda.set_stream(torch.cuda.Stream())
@@ -417,7 +425,7 @@ def run(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -430,6 +438,7 @@ def run(args):
         tot = torch.stack([counts[:S].sum(dtype=torch.int64), summ[:S, 0].sum()])
         want = n
     if distributed and fleet:
+        tot = tot.to(coll_dev)
         dist.all_reduce(tot)
     assert int(tot[0].item()) == want, f"summary counts sum {int(tot[0].item())} != {want}"
     if not fleet:
@@ -503,6 +512,9 @@ def run(args):
                                f"replicas x{world}"),
                "step": ("ingest + l5dh_merge (export, reduce-scatter, slice summaries)" if fleet else
                         "ingest (count+scan+bin1+bin2) + snapshot(reset, dense counts + summaries)")}
+        if distributed and backend != "nccl":
+            cfg["rehearsal"] = (f"{backend} rank harness, {world} ranks on {torch.cuda.device_count()} GPU(s): "
+                                "not a scaling number")
         if args.shard:
             cfg["shard"] = f"rank {pl['rank']} of {pl['world']}: series [{pl['first']}, {pl['first'] + S}), {n} samples"
         if streaming:
