@@ -39,6 +39,7 @@ constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
 #define L5DH_B2_ITEM 32768
 #endif
 constexpr uint32_t B2_ITEM = L5DH_B2_ITEM;  // target level-1 records per k_bin2 item
+static_assert(B2_ITEM >= 16384, "the plan's item map holds (2^30 / 16384 + 1024) items");
 
 // ------------------------------------------------------------------------
 // Count key of a valid sample: its tile, or for a split tile the column of its
@@ -318,9 +319,10 @@ __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series,
 // ------------------------------------------------------------------------
 // Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
 
-// Level 1.  Bins = the FS super-tiles (records of their non-split tiles, into
-// scratch1) and both halves of the ND split tiles (records straight into the
-// final layout: half 0 from the tile's start, half 1 after all half-0 records), plus a trash bin for sample slots with no sample (batch
+// Level 1.  Bins = the FS super-tiles (records of their non-direct tiles, into
+// scratch1) and two bins per direct tile (records straight into the final layout;
+// a split tile's half 0 from the tile's start, half 1 after all half-0 records; an
+// unsplit tile's bins share one range, the even bin's run first), plus a trash bin for sample slots with no sample (batch
 // tail, ids >= S: counted as errors by k_count) written to scratch1[n ..).  Both
 // arrays share the final layout's index space: slab g's records of direct tile t
 // start at tile_base[t] + pre[g][t]; its level-1 records of super-tile j at
@@ -348,6 +350,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
   uint2* dw = oc + BIN1_BINS;                                      // [1024] {direct bits, direct tiles before}
   uint8_t* hslot = reinterpret_cast<uint8_t*>(dw + 1024);          // [BIN1_BINS] hot slot of a bin (NHOT: none)
   uint32_t* hcnt = reinterpret_cast<uint32_t*>(hslot + BIN1_BINS); // [NHOT + 1][64] lane-private hot counters
+  uint32_t* dun = hcnt + (NHOT + 1) * 64;                          // [8] unsplit direct tiles (bit d)
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t NW = (F + 31) / 32;
   const uint32_t ND = plan[PLAN_ND];
@@ -392,10 +395,20 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
     v = wave_sum(v);
     if (lane == 0) oc[t >> 6] = make_uint2(0u, tile_base[t] + v);
   }
+  if (threadIdx.x < 8) dun[threadIdx.x] = 0u;
+  __syncthreads();
   for (uint32_t h = threadIdx.x; h < 2 * ND; h += NT) {  // direct tile h/2: half 0 from its start, half 1 after it
     const uint32_t si = plan[PLAN_DSI + (h >> 1)];
     const uint32_t t = plan[PLAN_DLIST + (h >> 1)];
-    const uint32_t at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + 2 * si + (h & 1u)];
+    uint32_t at;
+    if (si == NOKEY) {
+      // unsplit direct tile (counted per tile): both bins share the slab's one range,
+      // the odd bin's cursor is canonical (the bin scan places the even bin's run first)
+      at = tile_base[t] + prow[t];
+      if (h & 1u) atomicOr(&dun[h >> 6], 1u << ((h >> 1) & 31u));
+    } else {
+      at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + 2 * si + (h & 1u)];
+    }
     oc[FS + h] = make_uint2(0u, at | 0x80000000u);
   }
   if (threadIdx.x == 0) oc[TB] = make_uint2(0u, trash);
@@ -567,6 +580,15 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         oc[16 * lane + q].x = e;
         e += c[q];
       }
+      // unsplit direct tiles: this sub-chunk's run of the even bin, then the odd bin's,
+      // from the shared cursor (held by the odd bin: the advance below adds both counts)
+      for (uint32_t d = (uint32_t)lane; d < ND; d += 64)
+        if ((dun[d >> 5] >> (d & 31u)) & 1u) {
+          const uint32_t b0 = FS + 2 * d;
+          const uint32_t base = oc[b0 + 1].y;
+          oc[b0].y = base;
+          oc[b0 + 1].y = base + cnt[b0];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -609,7 +631,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 //   plan[2FS+1 .. 3FS]   hot non-split tiles of the super-tile (tile-in-ST, byte 0
 //                        and 1; 0xFF = none): >= 1/8 of its level-1 records
 //   plan[3FS+1 .. +NHOT] hot k_bin1 bins (>= 1/128 of all records, or ~0u)
-//   plan[PLAN_DBITS..]   this batch's split tiles (copy of slot `cur`)
+//   plan[PLAN_DBITS..]   this batch's direct tiles (bitmap, prefixes, list, split index)
 //   nxt                  the next batch's split set
 //   plan[PLAN_HINT..+1]  hot count columns for the next batch's k_count
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
@@ -625,21 +647,20 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   const uint32_t NS = cur[0];
   if (j < 33) lhd[j] = lhs[j] = 0;
   __syncthreads();
-  // direct tiles: split tiles of this batch with >= max(thr_min, 2^k) records;
-  // next split set: tiles with >= max(split_min, 2^k) records
-  if (dmax > 0)
-    for (uint32_t si = j; si < NS; si += 1024) {
-      const uint32_t v = coltot[cur[SPLIT_LIST + si]];
-      if (v >= thr_min && v > 0) atomicAdd(&lhd[31 - __clz((int)v)], 1u);
-    }
+  // direct tiles: tiles of this batch (split or not: the exact totals of k_count)
+  // with >= max(thr_min, 2^k) records; next split set: tiles with >= max(split_min,
+  // 2^k) records
+  (void)NS;
   {  // F <= 32768 tiles: a thread's <= 32 totals are loaded at once (one latency, not 32)
     constexpr int PF = 32;
     uint32_t tv[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) tv[k] = j + 1024u * k < F ? coltot[j + 1024u * k] : 0u;
 #pragma unroll
-    for (int k = 0; k < PF; ++k)
+    for (int k = 0; k < PF; ++k) {
       if (tv[k] >= split_min && tv[k] > 0) atomicAdd(&lhs[31 - __clz((int)tv[k])], 1u);
+      if (dmax > 0 && tv[k] >= thr_min && tv[k] > 0) atomicAdd(&lhd[31 - __clz((int)tv[k])], 1u);
+    }
   }
   __syncthreads();
   if (j < 2) {
@@ -695,8 +716,7 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
         if (v >= thr_s) {
           if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
         }
-        const bool split = ((tl < 32 ? c0 : c1) >> (tl & 31u)) & 1u;
-        if (split && v >= thr_d) {  // direct: no level-1 records
+        if (v >= thr_d) {  // direct: no level-1 records
           if (tl < 32) d0 |= 1u << tl; else d1 |= 1u << (tl - 32);
         } else {
           ctot += v;
@@ -739,6 +759,8 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   if (j < FS) {
     plan[j] = e;
     plan[FS + 1 + j] = gsz;
+    uint16_t* imap = reinterpret_cast<uint16_t*>(plan + PLAN_ITEMS);  // k_bin2: item -> super-tile, one load
+    for (uint32_t k = 0; k < nb; ++k) imap[e + k] = (uint16_t)j;
     plan[2 * FS + 1 + j] = hot;
     // this batch's direct tiles, their split index and half bins
     plan[PLAN_DBITS + 2 * j] = d0;
@@ -758,7 +780,8 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
         const uint32_t b = (uint32_t)(__ffs((int)w) - 1);
         w &= w - 1u;
         plan[PLAN_DLIST + di] = j * ST_TILES + 32u * q + b;
-        plan[PLAN_DSI + di] = sp + (uint32_t)__popc(cw & ((1u << b) - 1u));
+        // split index, or NOKEY: an unsplit direct tile (its two bins share its range)
+        plan[PLAN_DSI + di] = ((cw >> b) & 1u) ? sp + (uint32_t)__popc(cw & ((1u << b) - 1u)) : NOKEY;
         ++di;
       }
     }
@@ -788,8 +811,14 @@ __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32
   __syncthreads();  // the direct list is written
   for (uint32_t d = threadIdx.x; hot_bins && d < ndtot; d += 1024) {  // the direct tiles' half bins as hot-bin candidates
     const uint32_t si = plan[PLAN_DSI + d];
-    push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * d));
-    push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * d + 1));
+    if (si == NOKEY) {  // an unsplit direct tile: its records split between both bins by series bit 4
+      const unsigned long long h = coltot[plan[PLAN_DLIST + d]] / 2;
+      push((h << 11) | (FS + 2 * d));
+      push((h << 11) | (FS + 2 * d + 1));
+    } else {
+      push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * d));
+      push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * d + 1));
+    }
   }
   // grand total, the hot bins and the two biggest tiles (block reductions)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -882,13 +911,10 @@ __global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t C = F + COLS;
   const uint32_t item = blockIdx.x;
-  if (item >= plan[FS]) return;
-  uint32_t lo = 0, hi = FS;  // last j with plan[j] <= item
-  while (hi - lo > 1) {
-    const uint32_t m = (lo + hi) >> 1;
-    if (plan[m] <= item) lo = m; else hi = m;
-  }
-  const uint32_t j = lo;
+  // (both loads at once: entries past the batch's items are stale, never used)
+  const uint32_t nitems = plan[FS];
+  const uint32_t j = reinterpret_cast<const uint16_t*>(plan + PLAN_ITEMS)[item];
+  if (item >= nitems) return;
   const uint32_t gsz = plan[FS + 1 + j];
   const int g0 = (int)((item - plan[j]) * gsz);
   const int g1 = min(G, g0 + (int)gsz);

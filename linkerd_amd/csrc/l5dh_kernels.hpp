@@ -123,12 +123,14 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
                       int64_t* sumfix, bool vec, hipStream_t st);
 // Two-level partition: k_bin1 (slab -> super-tiles, LDS-sorted runs) + k_bin2
 // (super-tile -> tiles).  scratch1 holds n level-1 records.
-// Direct tiles (a subset of the split tiles, <= DIRECT_MAX): the two halves of each
-// bypass level 2 -- k_bin1 writes their records straight into the final layout.
+// Direct tiles (the biggest tiles of THIS batch, <= DIRECT_MAX, from k_count's exact
+// totals): two k_bin1 bins each (the halves of a split tile; for an unsplit tile
+// both share the tile's range) bypass level 2 -- k_bin1 writes their records
+// straight into the final layout.
 constexpr int DIRECT_MAX = 255;
 constexpr int BIN1_BINS = 1024;     // super-tiles (<= 512) + 2 x direct tiles + the trash bin
 // k_bin1 LDS for a sub-chunk of ch slots: stage, cnt, oc, direct words + prefixes, hot slots, hot counters
-constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4; }
+constexpr size_t bin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + BIN1_BINS + 9 * 64 * 4 + 32; }
 constexpr size_t BIN1_SCRATCH_PAD = 16384 + 16;  // scratch1 entries past n (k_bin1 trash bin, any sub-chunk size)
 // Ingest plan (device scratch of PLAN_WORDS u32), written by k_stplan:
 constexpr int PLAN_HINT = 2040;     // [4] hot count-table columns: hints for the next batch's k_count
@@ -139,7 +141,9 @@ constexpr int PLAN_DSI = 4352;      // [256] their split index
 constexpr int PLAN_ND = 4608;       // number of direct tiles
 constexpr int PLAN_HS = 4609;       // 1: one k_bin1 bin holds >= half the batch (lane-private hot slots pay)
 constexpr int PLAN_SPLIT = 8192;    // two split-set slots (this batch's, the next batch's)
-constexpr int PLAN_WORDS = PLAN_SPLIT + 2 * SPLIT_SLOT;
+constexpr int PLAN_ITEMS = PLAN_SPLIT + 2 * SPLIT_SLOT;  // u16 [level-2 item] -> its super-tile
+constexpr int PLAN_ITEMS_MAX = (1 << 30) / 16384 + 1024;  // batch / smallest B2_ITEM + FS + 1
+constexpr int PLAN_WORDS = PLAN_ITEMS + PLAN_ITEMS_MAX / 2;
 // Super-tile plan (level-2 items, direct bins, hot keys) for this batch's split
 // set `cur`: its direct tiles are the split tiles with records >= max(thr_min,
 // 2^k), k the smallest power keeping <= dmax tiles.  The next batch's split set

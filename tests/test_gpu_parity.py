@@ -211,6 +211,29 @@ def test_split_bins_one_bucket(oracle, value):
         _assert_summaries_equal(got, o.snapshot(reset=it == 1), f"capacity {it}")
 
 
+def test_unsplit_direct_tiles(oracle):
+    """Direct tiles come from THIS batch's exact tile totals: a hot set the previous
+    batch did not predict (no split tiles there) is binned straight into the final
+    layout by k_bin1, both series halves of a tile sharing one range per slab across
+    many 16K sub-chunks, then accumulated as big unsplit tiles."""
+    rng = np.random.default_rng(31)
+    S = 5000
+    eng = _engine(S, 2)
+    o = oracle.OracleHistograms(S)
+    for it, (lo, hi) in enumerate([(0, 0), (320, 448), (3000, 3007), (320, 448)]):
+        n_hot = 0 if hi == lo else 1_200_000
+        series = np.concatenate([rng.integers(lo, max(hi, lo + 1), n_hot), rng.integers(0, S, 800_000)]).astype(np.uint32)
+        rng.shuffle(series)
+        vals = np.exp(3 + rng.standard_normal(series.size)).astype(np.float32)
+        vals[::101] = rng.choice(EDGE_VALUES, size=vals[::101].size)
+        eng.ingest(series, vals)
+        o.ingest(series, vals)
+        reset = it != 1
+        got, counts = eng.snapshot(reset=reset, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"batch {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=reset), f"unsplit direct {it}")
+
+
 def test_big_tile_bins_past_u16(oracle):
     """Big tiles outside the split set (k_accum_hot: whole-tile u16 bins): one bin of
     a 2^18-record item passes 2^15 many times and hands each 2^15 to the state row;
