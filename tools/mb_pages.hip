@@ -75,7 +75,8 @@ constexpr size_t LDS_BYTES = (size_t)CH1 * 8 + 7 * BINS * 4 + 16;
 __global__ __launch_bounds__(NT, 1) void k_bin1p(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                  size_t n, size_t per, uint32_t S, uint32_t P, uint32_t pool_pages,
                                                  uint32_t* __restrict__ pool, uint2* __restrict__ plog,
-                                                 uint32_t* __restrict__ nlog, uint2* __restrict__ tailpg) {
+                                                 uint32_t* __restrict__ nlog, uint2* __restrict__ tailpg,
+                                                 const uint32_t* __restrict__ dst0) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint2* stage = reinterpret_cast<uint2*>(smem);
   uint32_t* cnt = smem + 2 * CH1;
@@ -90,9 +91,10 @@ __global__ __launch_bounds__(NT, 1) void k_bin1p(const uint32_t* __restrict__ se
   const uint32_t TB = FS + 2 * ND;
   const uint32_t g = blockIdx.x;
   const uint32_t pool0 = g * pool_pages;  // first page of this slab's pool
+  // dst0 (comparison layouts): exact per-(slab, bin) start positions, no pages
   for (uint32_t b = threadIdx.x; b < BINS; b += NT) {
     cnt[b] = 0;
-    pg[b] = 0;
+    pg[b] = dst0 ? dst0[(size_t)blockIdx.x * BINS + b] : 0u;
     fill[b] = P;  // no page yet: the first run allocates
   }
   if (threadIdx.x == 0) cur[0] = cur[1] = 0;
@@ -144,6 +146,12 @@ __global__ __launch_bounds__(NT, 1) void k_bin1p(const uint32_t* __restrict__ se
     for (uint32_t b = threadIdx.x; b < BINS; b += NT) {
       const uint32_t c = cnt[b];
       if (!c) continue;
+      if (dst0) {  // exact placement: the run continues at the bin's cursor
+        dA[b] = pg[b];
+        room[b] = 0xFFFFFFFFu;
+        pg[b] += c;
+        continue;
+      }
       const uint32_t rm = P - fill[b];
       dA[b] = pg[b] + fill[b];
       room[b] = rm;
@@ -177,6 +185,19 @@ __global__ __launch_bounds__(NT, 1) void k_bin1p(const uint32_t* __restrict__ se
   }
   for (uint32_t b = threadIdx.x; b < BINS; b += NT) tailpg[(size_t)g * BINS + b] = make_uint2(pg[b], fill[b]);
   if (threadIdx.x == 0) nlog[g] = cur[1];
+}
+
+// per-(slab, bin) counts of the same slabs (for the exact comparison layouts)
+__global__ __launch_bounds__(1024) void k_cnt_slab_bins(const uint32_t* __restrict__ series, size_t n, size_t per,
+                                                        uint32_t S, uint32_t* __restrict__ out) {
+  __shared__ uint32_t c[BINS];
+  const uint32_t FS = (S + 2047) / 2048, TB = FS + 2 * ND;
+  for (int b = threadIdx.x; b < BINS; b += 1024) c[b] = 0;
+  __syncthreads();
+  const size_t lo = (size_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  for (size_t i = lo + threadIdx.x; i < hi; i += 1024) atomicAdd(&c[bin_of(series[i], S, FS, TB)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < BINS; b += 1024) out[(size_t)blockIdx.x * BINS + b] = c[b];
 }
 
 // ---- checks ----
@@ -251,25 +272,73 @@ int main(int argc, char** argv) {
   if (l5ds_gen_zipf(series, values, n, S, dcdf, 3, 0.8, 0, 0, nullptr)) return 1;
   CHK(hipDeviceSynchronize());
   CHK(hipFuncSetAttribute((const void*)k_bin1p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES));
+  // comparison layouts with exact placement (the engine's k_count provides it):
+  // bin-major = the engine's level-1 layout (a bin's region, slabs in order inside
+  // it); slab-major = each slab's own region, bins in order inside it
+  uint32_t *cnts, *dbm, *dsm;
+  CHK(hipMalloc(&cnts, (size_t)G * BINS * 4));
+  CHK(hipMalloc(&dbm, (size_t)G * BINS * 4));
+  CHK(hipMalloc(&dsm, (size_t)G * BINS * 4));
+  hipLaunchKernelGGL(k_cnt_slab_bins, dim3(G), dim3(1024), 0, 0, series, n, per, S, cnts);
+  std::vector<uint32_t> hc((size_t)G * BINS), hb((size_t)G * BINS), hs((size_t)G * BINS);
+  CHK(hipMemcpy(hc.data(), cnts, hc.size() * 4, hipMemcpyDeviceToHost));
+  {
+    uint64_t x = 0;
+    for (int bb = 0; bb < BINS; ++bb)
+      for (int g = 0; g < G; ++g) {
+        hb[(size_t)g * BINS + bb] = (uint32_t)x;
+        x += hc[(size_t)g * BINS + bb];
+      }
+    x = 0;
+    for (int g = 0; g < G; ++g)
+      for (int bb = 0; bb < BINS; ++bb) {
+        hs[(size_t)g * BINS + bb] = (uint32_t)x;
+        x += hc[(size_t)g * BINS + bb];
+      }
+  }
+  CHK(hipMemcpy(dbm, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  CHK(hipMemcpy(dsm, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+  // bin-major with every (slab, bin) segment start aligned to A records (gaps between)
+  const uint32_t AL[2] = {16, 1024};
+  uint32_t* dal[2];
+  for (int q = 0; q < 2; ++q) {
+    uint64_t x = 0;
+    for (int bb = 0; bb < BINS; ++bb)
+      for (int g = 0; g < G; ++g) {
+        const uint32_t c = hc[(size_t)g * BINS + bb];
+        if (c) x = (x + AL[q] - 1) / AL[q] * AL[q];
+        hb[(size_t)g * BINS + bb] = (uint32_t)x;
+        x += c;
+      }
+    if (x + 20000 > (uint64_t)G * pool_pages * P) { printf("aligned layout exceeds the pool\n"); return 1; }
+    CHK(hipMalloc(&dal[q], (size_t)G * BINS * 4));
+    CHK(hipMemcpy(dal[q], hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  }
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
-  double best = 1e30, sum = 0;
-  for (int r = 0; r < reps + 1; ++r) {
-    CHK(hipEventRecord(a));
-    hipLaunchKernelGGL(k_bin1p, dim3(G), dim3(NT), LDS_BYTES, 0, series, values, n, per, S, P, pool_pages, pool, plog,
-                       nlog, tailpg);
-    CHK(hipEventRecord(b));
-    CHK(hipEventSynchronize(b));
-    float ms;
-    CHK(hipEventElapsedTime(&ms, a, b));
-    if (r > 0) {  // the first launch is a warmup (first touch of the pool)
-      best = ms < best ? ms : best;
-      sum += ms;
+  const int NM = 5;
+  const char* names[NM] = {"pages", "bin-major (engine layout)", "slab-major", "bin-major, 64-B aligned", "bin-major, 4-KB aligned"};
+  const uint32_t* tabs[NM] = {nullptr, dbm, dsm, dal[0], dal[1]};
+  double best[NM], sum[NM];
+  for (int m = 0; m < NM; ++m) best[m] = 1e30, sum[m] = 0;
+  for (int r = 0; r < reps + 1; ++r)
+    for (int m = NM - 1; m >= 0; --m) {  // pages last: its pool is what the checks read
+      CHK(hipEventRecord(a));
+      hipLaunchKernelGGL(k_bin1p, dim3(G), dim3(NT), LDS_BYTES, 0, series, values, n, per, S, P, pool_pages, pool,
+                         plog, nlog, tailpg, tabs[m]);
+      CHK(hipEventRecord(b));
+      CHK(hipEventSynchronize(b));
+      float ms;
+      CHK(hipEventElapsedTime(&ms, a, b));
+      if (r > 0) {  // the first round is a warmup (first touch of the pool)
+        best[m] = ms < best[m] ? ms : best[m];
+        sum[m] += ms;
+      }
     }
-  }
-  printf("k_bin1p: mean %.4f ms, best %.4f ms over %d launches (%.1f GB/s of input)\n", sum / reps, best, reps,
-         8.0 * n / (sum / reps) / 1e6);
+  for (int m = 0; m < NM; ++m)
+    printf("k_bin1p %-26s mean %.4f ms, best %.4f ms over %d launches (%.1f GB/s of input)\n", names[m], sum[m] / reps,
+           best[m], reps, 8.0 * n / (sum[m] / reps) / 1e6);
   // checks
   CHK(hipMemset(chk, 0, (2 * BINS + 2) * 8));
   unsigned long long* bins_in = chk;
