@@ -200,7 +200,12 @@ struct l5dh_ctx {
   int max_seg = 4;
   // staging
   DevBuf scratch1;  // level-1 records of the two-level partition
-  int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level
+  // paged ingest (bin mode 3): page pools, allocation logs, last pages, directory, level-2 counts
+  DevBuf pool, plog, tailpg, pdir, cnt2;
+  uint32_t* d_nlog = nullptr;   // [512] log entries per slab
+  uint32_t* d_pd = nullptr;     // [PD_WORDS]
+  uint32_t* d_ptot = nullptr;   // [F] tile totals of the paged final layout
+  int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level, 3 paged two-level
   uint32_t direct_max = DIRECT_MAX;  // tiles k_bin1 may write in final form (0: none)
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
@@ -492,6 +497,65 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   per = (per + 3) & ~(size_t)3;
   G = (int)((n + per - 1) / per);
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
+  if (c->bin_mode == 3) {  // paged: no counting pass (l5dh_paged.hip)
+    const size_t pp = paged_pool_pages(per);
+    if ((double)G * (double)pp * PAGE >= 4294967296.0) return fail(c, -EINVAL, "paged ingest: batch too large");
+    int r = ensure(c, c->pool, (size_t)G * pp * PAGE * 4);
+    if (!r) r = ensure(c, c->plog, (size_t)G * pp * 8);
+    if (!r) r = ensure(c, c->tailpg, (size_t)G * PG_BINS * 8);
+    if (!r) r = ensure(c, c->pdir, (size_t)G * pp * 8);
+    if (!r) r = ensure(c, c->cnt2, ((size_t)G * pp / KP + 1024) * 64 * 4);
+    if (r) return r;
+    const uint32_t FS = (c->F + 63) / 64;
+    PagedArgs a{};
+    a.series = ds;
+    a.values = dv;
+    a.n = n;
+    a.per = per;
+    a.G = G;
+    a.num_cu = c->num_cu;
+    a.S = c->S;
+    a.F = c->F;
+    a.plan = c->d_b2plan;
+    a.tb = tables(c);
+    a.state = state(c);
+    a.err = c->d_err;
+    a.pool_pages = (uint32_t)pp;
+    a.pool = static_cast<uint32_t*>(c->pool.p);
+    a.plog = static_cast<uint2*>(c->plog.p);
+    a.nlog = c->d_nlog;
+    a.tailpg = static_cast<uint2*>(c->tailpg.p);
+    a.pd = c->d_pd;
+    a.dir = static_cast<uint2*>(c->pdir.p);
+    a.cnt2 = static_cast<uint32_t*>(c->cnt2.p);
+    a.tot = c->d_ptot;
+    a.tile_base = sg.tbase;
+    a.records = static_cast<uint32_t*>(sg.recs.p);
+    a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
+    a.dmax = std::min<uint32_t>(c->direct_max, std::min<uint32_t>(DIRECT_MAX, ((uint32_t)PG_BINS - 1 - FS) / 2));
+    a.vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
+    {
+      KTimer kt(c, L5DH_K_BIN);
+      HIPCHK(c, launch_paged_ingest(a, 0, c->stream));
+    }
+    {
+      KTimer kt(c, L5DH_K_SCAN);
+      HIPCHK(c, launch_paged_ingest(a, 1, c->stream));
+      HIPCHK(c, launch_seginfo(c->d_nosplit, c->d_tile_tot, c->F, sg.sinfo, c->stream));
+    }
+    {
+      KTimer kt(c, L5DH_K_HOT);
+      HIPCHK(c, launch_paged_ingest(a, 2, c->stream));
+    }
+    {
+      KTimer kt(c, L5DH_K_BIN2);
+      HIPCHK(c, launch_paged_ingest(a, 3, c->stream));
+    }
+    sg.n = n;
+    c->nseg++;
+    HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  }
   const bool two_level = c->bin_mode != 1;
   // split set of this batch (chosen from the previous batch's tile totals) and of the next
   uint32_t* split_slot = c->d_b2plan + PLAN_SPLIT;
@@ -806,7 +870,9 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   // CU (LDS-bound), so a second round of slabs only adds table rows (measured: 2 x CUs
   // is ~1.4 % slower on C2 and no faster on C3)
   c->G_max = std::max(1, std::min(c->num_cu, 512));
-  if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
+  if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess ||
+      set_paged_attributes() != hipSuccess)
+    return bail(-EIO);
   if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
@@ -824,7 +890,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_tile_tot, (F + COLS) * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) &&
             mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
-            mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT);
+            mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT) && mal((void**)&c->d_nlog, 512 * 4) &&
+            mal((void**)&c->d_pd, 4 * PD_WORDS) && mal((void**)&c->d_ptot, F * 4);
   for (int j = 0; ok && j < MAX_SEG; ++j)
     ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4) && mal((void**)&c->segs[j].sinfo, sinfo_words(c->F) * 4);
   if (!ok) {
@@ -854,6 +921,9 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
       hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * PLAN_SPLIT) != hipSuccess ||
       hipMemset(c->d_b2plan + PLAN_SPLIT, 0, 4 * 2 * SPLIT_SLOT) != hipSuccess ||
+      // no direct tiles before the first batch (the paged path reads the previous batch's)
+      hipMemset(c->d_b2plan + PLAN_DBITS, 0, 4 * 2048) != hipSuccess ||
+      hipMemset(c->d_b2plan + PLAN_ND, 0, 4) != hipSuccess ||
       hipMemset(c->d_nosplit, 0, 4 * SPLIT_SLOT) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
@@ -871,7 +941,8 @@ int l5dh_close(l5dh_ctx* c) {
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
-                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan, c->d_tile_flags, c->d_nosplit};
+                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan, c->d_tile_flags, c->d_nosplit,
+                  c->d_nlog, c->d_pd, c->d_ptot};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
@@ -883,7 +954,8 @@ int l5dh_close(l5dh_ctx* c) {
   DevBuf* bufs[] = {&c->scratch1,      &c->hot_item,        &c->split_item,   &c->stage_series, &c->stage_values,
                     &c->stage_summ,    &c->stage_counts,    &c->stage_totals, &c->stage_in_counts,
                     &c->stage_in_totals, &c->ring_series,   &c->ring_values,  &c->merge_counts,  &c->merge_totals,
-                    &c->recv_counts,   &c->recv_totals};
+                    &c->recv_counts,   &c->recv_totals,     &c->pool,         &c->plog,         &c->tailpg,
+                    &c->pdir,          &c->cnt2};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->h_header) hipHostFree(c->h_header);
@@ -1097,7 +1169,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       c->max_seg = (int)v;
       return 0;
     case L5DH_PARAM_BIN_MODE:
-      if (v < 0 || v > 2) return fail(c, -EINVAL, "bin mode must be 0 (auto), 1 (single) or 2 (two-level)");
+      if (v < 0 || v > 3) return fail(c, -EINVAL, "bin mode must be 0 (auto), 1 (single), 2 (two-level) or 3 (paged)");
       c->bin_mode = (int)v;
       return 0;
     case L5DH_PARAM_DIRECT_MAX:

@@ -179,6 +179,45 @@ hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total
 // Copy n (series, value) pairs from device-visible pinned host memory (zero-copy).
 hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
                              hipStream_t st);
+// ---- paged ingest (L5DH_PARAM_BIN_MODE 3, l5dh_paged.hip) ----
+// k_bin1's LDS counting sort into CU-private pools of PAGE-record pages (no counting
+// pass); direct half-tiles folded into state rows at ingest; level 2 of the other
+// tiles counted and placed from a page directory.  Items = KP pages.
+constexpr int PG_BINS = BIN1_BINS;
+constexpr uint32_t PAGE = 4096;
+constexpr uint32_t KP = 8;
+constexpr int PD_WORDS = 5136;  // per-bin page / record counts, bases, item bases, header
+constexpr size_t PFOLD_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + LUT2_N * 8 + (2 * DIRECT_MAX + 2) * 4;
+constexpr size_t P2PLACE_LDS = (size_t)2 * PAGE * 8 + 3 * 64 * 4 + 513 * 4;
+struct PagedArgs {
+  const uint32_t* series;
+  const float* values;
+  size_t n, per;
+  int G, num_cu;
+  uint32_t S, F;
+  uint32_t* plan;        // the ingest plan: this batch's direct tiles in, the next batch's out
+  Tables tb;
+  State state;
+  uint32_t* err;
+  uint32_t pool_pages;   // pages per slab
+  uint32_t* pool;        // [G * pool_pages * PAGE] records
+  uint2* plog;           // [G * pool_pages] allocation log
+  uint32_t* nlog;        // [G]
+  uint2* tailpg;         // [G * PG_BINS] last page and its fill
+  uint32_t* pd;          // [PD_WORDS]
+  uint2* dir;            // [G * pool_pages] page directory
+  uint32_t* cnt2;        // [level-2 items * 64]
+  uint32_t* tot;         // [F] tile totals of the final layout
+  uint32_t* tile_base;   // [F + 1] the segment's tile offsets
+  uint32_t* records;     // the segment's final layout
+  uint32_t thr_min, dmax;
+  bool vec;
+};
+size_t paged_pool_pages(size_t per);
+hipError_t set_paged_attributes();
+// phase 0: level 1, 1: page directory, 2: direct fold, 3: level 2 (+ the next direct set)
+hipError_t launch_paged_ingest(const PagedArgs& a, int phase, hipStream_t st);
+
 hipError_t set_ingest_attributes();
 hipError_t set_snapshot_attributes();
 hipError_t set_snapshot_debug(int dbg);

@@ -31,7 +31,8 @@ def _engine(S, bin_mode=0, stage=0):
     return e
 
 
-BIN_MODES = pytest.mark.parametrize("bin_mode", [1, 2], ids=["single", "twolevel"])
+BIN_MODES = pytest.mark.parametrize("bin_mode", [1, 2, 3], ids=["single", "twolevel", "paged"])
+TWO_LEVEL = pytest.mark.parametrize("mode", [2, 3], ids=["twolevel", "paged"])
 
 
 def _assert_summaries_equal(got, want, label=""):
@@ -97,15 +98,16 @@ def test_edge_values_every_series(oracle, bin_mode):
     _assert_summaries_equal(got, o.snapshot(), "edge")
 
 
+@TWO_LEVEL
 @pytest.mark.parametrize("stage", [0, None, 50_000], ids=["unstaged", "ring", "smallring"])
 @pytest.mark.parametrize("reset", [False, True])
-def test_multi_batch_and_cumulative_snapshots(oracle, reset, stage):
+def test_multi_batch_and_cumulative_snapshots(oracle, reset, stage, mode):
     """Several ingests (segments + folds, or the staging ring flushed when full and
     at the snapshot) and snapshots with / without reset (Prometheus P2 is
     cumulative: snapshot() without reset, PrometheusTelemeterTest.scala:70-86)."""
     rng = np.random.default_rng(5 + reset)
     S = 333
-    eng = _engine(S, stage=stage)
+    eng = _engine(S, mode, stage=stage)
     eng.set_param(N.PARAM_MAX_SEGMENTS, 2)
     o = oracle.OracleHistograms(S)
     for it in range(3):
@@ -151,15 +153,16 @@ def test_hot_tile_split_path(oracle, bin_mode):
     _assert_summaries_equal(got, o.snapshot(reset=False)[:40], "hot fold")
 
 
+@TWO_LEVEL
 @pytest.mark.parametrize("direct_max", [0, 2, 255])
-def test_split_tiles_across_batches(oracle, direct_max):
+def test_split_tiles_across_batches(oracle, direct_max, mode):
     """Split tiles: the previous batch's big tiles are counted and laid out per
     half-tile (direct ones by k_bin1, the rest through k_bin2).  Batches with
     different hot tiles leave a tile split in some pending segments only (mixed
     items) and in all of them (split items)."""
     rng = np.random.default_rng(21 + direct_max)
     S = 4000
-    eng = _engine(S, 2)
+    eng = _engine(S, mode)
     eng.set_param(N.PARAM_COLD_LIMIT, 500)
     eng.set_param(N.PARAM_HOT_CHUNK, 5000)
     eng.set_param(N.PARAM_MAX_SEGMENTS, 3)
@@ -211,14 +214,15 @@ def test_split_bins_one_bucket(oracle, value):
         _assert_summaries_equal(got, o.snapshot(reset=it == 1), f"capacity {it}")
 
 
-def test_unsplit_direct_tiles(oracle):
+@TWO_LEVEL
+def test_unsplit_direct_tiles(oracle, mode):
     """Direct tiles come from THIS batch's exact tile totals: a hot set the previous
     batch did not predict (no split tiles there) is binned straight into the final
     layout by k_bin1, both series halves of a tile sharing one range per slab across
     many 16K sub-chunks, then accumulated as big unsplit tiles."""
     rng = np.random.default_rng(31)
     S = 5000
-    eng = _engine(S, 2)
+    eng = _engine(S, mode)
     o = oracle.OracleHistograms(S)
     for it, (lo, hi) in enumerate([(0, 0), (320, 448), (3000, 3007), (320, 448)]):
         n_hot = 0 if hi == lo else 1_200_000
@@ -234,13 +238,14 @@ def test_unsplit_direct_tiles(oracle):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"unsplit direct {it}")
 
 
-def test_big_tile_bins_past_u16(oracle):
+@TWO_LEVEL
+def test_big_tile_bins_past_u16(oracle, mode):
     """Big tiles outside the split set (k_accum_hot: whole-tile u16 bins): one bin of
     a 2^18-record item passes 2^15 many times and hands each 2^15 to the state row;
     a clean and a dirty tile, and a hot set that moves between batches."""
     rng = np.random.default_rng(17)
     S = 100
-    eng = _engine(S, 2)
+    eng = _engine(S, mode)
     o = oracle.OracleHistograms(S)
     plan = [(0, 7.0, 300_000, False), (40, 1_000_000.0, 200_000, False), (0, 113.0, 70_000, True),
             (70, 2_000_000.0, 280_000, True)]
@@ -371,15 +376,16 @@ def test_zipf_series_space_1m(oracle, bin_mode):
     assert counts.sum() == series.size
 
 
+@TWO_LEVEL
 @pytest.mark.parametrize("gmax", [1, 3, 7, 512])
-def test_slab_counts_bitexact(oracle, gmax):
+def test_slab_counts_bitexact(oracle, gmax, mode):
     """Ingest with G = min(max_slabs, n / 8192) slabs (default: one per CU): the
     per-(slab, column) prefixes, level-1 cursors and level-2 slab ranges must place
     every record exactly for any slab count, including one slab and odd counts.
     Two Zipf batches, so the second runs with split and direct tiles."""
     rng = np.random.default_rng(100 + gmax)
     S, n = 5000, 1_500_000
-    eng = _engine(S, 2)
+    eng = _engine(S, mode)
     eng.set_param(N.PARAM_MAX_SLABS, gmax)
     o = oracle.OracleHistograms(S)
     for _ in range(2):
