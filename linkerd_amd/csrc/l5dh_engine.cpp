@@ -205,6 +205,7 @@ struct l5dh_ctx {
   uint32_t* d_nlog = nullptr;   // [512] log entries per slab
   uint32_t* d_pd = nullptr;     // [PD_WORDS]
   uint32_t* d_ptot = nullptr;   // [F] tile totals of the paged final layout
+  uint32_t* d_pcount = nullptr; // [F] sampled ids per tile (k_psample; zeroed by k_pselect)
   int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level, 3 paged two-level
   uint32_t direct_max = DIRECT_MAX;  // tiles k_bin1 may write in final form (0: none)
   int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
@@ -529,6 +530,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     a.dir = static_cast<uint2*>(c->pdir.p);
     a.cnt2 = static_cast<uint32_t*>(c->cnt2.p);
     a.tot = c->d_ptot;
+    a.pcount = c->d_pcount;
     a.tile_base = sg.tbase;
     a.records = static_cast<uint32_t*>(sg.recs.p);
     a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
@@ -891,7 +893,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) &&
             mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
             mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT) && mal((void**)&c->d_nlog, 512 * 4) &&
-            mal((void**)&c->d_pd, 4 * PD_WORDS) && mal((void**)&c->d_ptot, F * 4);
+            mal((void**)&c->d_pd, 4 * PD_WORDS) && mal((void**)&c->d_ptot, F * 4) &&
+            mal((void**)&c->d_pcount, F * 4);
   for (int j = 0; ok && j < MAX_SEG; ++j)
     ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4) && mal((void**)&c->segs[j].sinfo, sinfo_words(c->F) * 4);
   if (!ok) {
@@ -924,7 +927,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
       // no direct tiles before the first batch (the paged path reads the previous batch's)
       hipMemset(c->d_b2plan + PLAN_DBITS, 0, 4 * 2048) != hipSuccess ||
       hipMemset(c->d_b2plan + PLAN_ND, 0, 4) != hipSuccess ||
-      hipMemset(c->d_nosplit, 0, 4 * SPLIT_SLOT) != hipSuccess ||
+      hipMemset(c->d_nosplit, 0, 4 * SPLIT_SLOT) != hipSuccess || hipMemset(c->d_pcount, 0, F * 4) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
   *out = c;
@@ -942,7 +945,7 @@ int l5dh_close(l5dh_ctx* c) {
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
                   c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan, c->d_tile_flags, c->d_nosplit,
-                  c->d_nlog, c->d_pd, c->d_ptot};
+                  c->d_nlog, c->d_pd, c->d_ptot, c->d_pcount};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {

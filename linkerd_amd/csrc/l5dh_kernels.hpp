@@ -184,11 +184,11 @@ hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* d
 // pass); direct half-tiles folded into state rows at ingest; level 2 of the other
 // tiles counted and placed from a page directory.  Items = KP pages.
 constexpr int PG_BINS = BIN1_BINS;
-constexpr uint32_t PAGE = 4096;
-constexpr uint32_t KP = 8;
+constexpr uint32_t PAGE = 1024;  // records per page (4 KB): a cold bin's slab run fills most of one
+constexpr uint32_t KP = 32;     // pages per item (32K records)
 constexpr int PD_WORDS = 5136;  // per-bin page / record counts, bases, item bases, header
 constexpr size_t PFOLD_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + LUT2_N * 8 + (2 * DIRECT_MAX + 2) * 4;
-constexpr size_t P2PLACE_LDS = (size_t)2 * PAGE * 8 + 3 * 64 * 4 + 513 * 4;
+constexpr size_t P2PLACE_LDS = (size_t)8192 * 8 + 3 * 64 * 4 + 513 * 4;
 struct PagedArgs {
   const uint32_t* series;
   const float* values;
@@ -208,6 +208,7 @@ struct PagedArgs {
   uint2* dir;            // [G * pool_pages] page directory
   uint32_t* cnt2;        // [level-2 items * 64]
   uint32_t* tot;         // [F] tile totals of the final layout
+  uint32_t* pcount;      // [F] sampled ids per tile (zero between batches)
   uint32_t* tile_base;   // [F + 1] the segment's tile offsets
   uint32_t* records;     // the segment's final layout
   uint32_t thr_min, dmax;
@@ -215,7 +216,7 @@ struct PagedArgs {
 };
 size_t paged_pool_pages(size_t per);
 hipError_t set_paged_attributes();
-// phase 0: level 1, 1: page directory, 2: direct fold, 3: level 2 (+ the next direct set)
+// phase 0: direct set (sampled) + level 1, 1: page directory, 2: direct fold, 3: level 2
 hipError_t launch_paged_ingest(const PagedArgs& a, int phase, hipStream_t st);
 
 hipError_t set_ingest_attributes();

@@ -2,6 +2,8 @@
 // writes into CU-private page pools, so no counting pass precedes it (DESIGN.md
 // §6c; the layouts measured in profiles/r02m_pages).
 //
+//   k_psample     this batch's tile sizes estimated from 2^20 sampled ids
+//   k_pselect     this batch's direct tiles (the biggest estimated, as k_stplan picks)
 //   k_pbin1       level 1: LDS counting sort of 16K-sample sub-chunks by bin (FS
 //                 super-tiles, two half-bins per direct tile, a trash bin); a bin's run
 //                 fills its current page and spills into consecutive fresh pages of
@@ -14,11 +16,10 @@
 //                 16 series per item, flushed with global atomics (as k_accum_split)
 //   k_p2count     level-2 items: records per tile of the super-tile
 //   k_p2scan_a    per super-tile: exclusive prefixes over its items, tile totals
-//   k_p2scan_b    tile_base of the final layout; the next batch's direct tiles
+//   k_p2scan_b    tile_base of the final layout
 //   k_p2place     level 2: items re-read, LDS-sorted by tile, written to the final layout
 //
-// The direct tiles of a batch are chosen from the previous batch's tile totals
-// (k_p2scan_b); their records never reach the final layout (the snapshot sees them
+// The direct tiles of a batch are chosen from a sample of its own ids; their records never reach the final layout (the snapshot sees them
 // as dirty tiles).  All other tiles' records are laid out per tile exactly as the
 // two-level path lays them out (split tiles: none), so the snapshot is unchanged.
 #include "l5dh_device.hpp"
@@ -182,20 +183,28 @@ constexpr int PD_PAGES = 0, PD_RECS = PG_BINS, PD_BASE = 2 * PG_BINS, PD_CUR = 3
               PD_DITEM = 4 * PG_BINS + 1, PD_LITEM = PD_DITEM + 2 * DIRECT_MAX + 2, PD_HDR = PD_LITEM + 514;
 static_assert(PD_HDR + 2 <= PD_WORDS, "page directory header");
 
+// Per slab (one workgroup): pages and records per bin summed in LDS, then one global
+// atomic per (slab, bin) -- a hot bin gets hundreds of log entries per slab, and
+// same-address global atomics serialize.
 __global__ __launch_bounds__(256) void k_pdir_count(const uint2* __restrict__ plog, const uint32_t* __restrict__ nlog,
                                                     const uint2* __restrict__ tailpg, uint32_t pool_pages,
                                                     uint32_t* __restrict__ pd) {
+  __shared__ uint32_t lp[PG_BINS], lr[PG_BINS];
   const uint32_t g = blockIdx.x;
   const uint32_t ne = nlog[g];
+  for (uint32_t b = threadIdx.x; b < PG_BINS; b += 256) lp[b] = lr[b] = 0;
+  __syncthreads();
   for (uint32_t i = threadIdx.x; i < ne; i += 256) {
     const uint2 e = plog[(size_t)g * pool_pages + i];
-    const uint32_t b = e.y & 0xFFFFu, np = e.y >> 16;
-    atomicAdd(&pd[PD_PAGES + b], np);
-    atomicAdd(&pd[PD_RECS + b], np * PAGE);
+    atomicAdd(&lp[e.y & 0xFFFFu], e.y >> 16);
   }
+  __syncthreads();
   for (uint32_t b = threadIdx.x; b < PG_BINS; b += 256) {
+    const uint32_t np = lp[b];
+    if (!np) continue;
     const uint2 t = tailpg[(size_t)g * PG_BINS + b];
-    if (t.x != 0xFFFFFFFFu) atomicSub(&pd[PD_RECS + b], PAGE - t.y);  // the last page's unused slots
+    atomicAdd(&pd[PD_PAGES + b], np);
+    atomicAdd(&pd[PD_RECS + b], np * PAGE - (PAGE - t.y));  // the last page's unused slots
   }
 }
 
@@ -225,15 +234,28 @@ __global__ __launch_bounds__(1024) void k_pdir_scan(uint32_t F, const uint32_t* 
 }
 
 // The page directory: dir[base[b] ..) = {page, records in it} of bin b, any order.
+// Per slab: its pages per bin (LDS), one global reservation per (slab, bin), then
+// the entries placed through LDS cursors.
 __global__ __launch_bounds__(256) void k_pdir_fill(const uint2* __restrict__ plog, const uint32_t* __restrict__ nlog,
                                                    const uint2* __restrict__ tailpg, uint32_t pool_pages,
                                                    uint32_t* __restrict__ pd, uint2* __restrict__ dir) {
+  __shared__ uint32_t lp[PG_BINS];
   const uint32_t g = blockIdx.x;
   const uint32_t ne = nlog[g];
+  for (uint32_t b = threadIdx.x; b < PG_BINS; b += 256) lp[b] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < ne; i += 256) {
+    const uint2 e = plog[(size_t)g * pool_pages + i];
+    atomicAdd(&lp[e.y & 0xFFFFu], e.y >> 16);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < PG_BINS; b += 256)
+    if (lp[b]) lp[b] = pd[PD_BASE + b] + atomicAdd(&pd[PD_CUR + b], lp[b]);
+  __syncthreads();
   for (uint32_t i = threadIdx.x; i < ne; i += 256) {
     const uint2 e = plog[(size_t)g * pool_pages + i];
     const uint32_t b = e.y & 0xFFFFu, np = e.y >> 16;
-    const uint32_t at = pd[PD_BASE + b] + atomicAdd(&pd[PD_CUR + b], np);
+    const uint32_t at = atomicAdd(&lp[b], np);
     const uint2 t = tailpg[(size_t)g * PG_BINS + b];
     for (uint32_t q = 0; q < np; ++q) {
       const uint32_t page = e.x + q;
@@ -278,27 +300,30 @@ __device__ __forceinline__ uint32_t upper_index(const uint32_t* __restrict__ bas
   return lo;
 }
 
-// Records of an item's pages: each page holds <= PAGE = 4 x WG records, so every
-// thread loads one 16-B group per page, all KP loads issued at once.
+// Records of an item's pages (<= KP pages of PAGE records = IR groups of 4 per
+// thread): thread t takes groups t, t + WG, ...; the page entries are wave-uniform
+// (scalar loads), and every load is issued before any record is used (no branches:
+// a group past the item or past its page's fill reads a valid page and is masked).
+constexpr int IR = (int)(KP * PAGE / 4 / WG);
 template <class Fn>
 __device__ __forceinline__ void item_records(const uint32_t* __restrict__ pool, const uint2* __restrict__ dir,
                                              uint32_t p0, uint32_t p1, Fn&& fn) {
-  static_assert(PAGE == 4 * WG, "one 16-B group per thread and page");
-  uint4 x[KP];
-  uint32_t m[KP];
+  static_assert(KP * PAGE % (4 * WG) == 0 && (PAGE / 4) % 64 == 0, "whole waves per page");
+  p0 = __builtin_amdgcn_readfirstlane(p0);
+  p1 = __builtin_amdgcn_readfirstlane(p1);
+  uint4 x[IR];
+  uint32_t m[IR];
 #pragma unroll
-  for (uint32_t q = 0; q < KP; ++q) {
-    m[q] = 0;
-    x[q] = make_uint4(0u, 0u, 0u, 0u);
-    if (p0 + q < p1) {
-      const uint2 e = dir[p0 + q];
-      const uint32_t o = 4u * threadIdx.x;
-      m[q] = e.y > o ? min(4u, e.y - o) : 0u;  // valid records of this thread's group
-      if (m[q]) x[q] = *reinterpret_cast<const uint4*>(pool + (size_t)e.x * PAGE + o);
-    }
+  for (int q = 0; q < IR; ++q) {
+    const uint32_t gi = (uint32_t)q * WG + threadIdx.x;
+    const uint32_t pi = p0 + gi / (PAGE / 4);  // wave-uniform: a wave's 64 groups are in one page
+    const uint2 e = dir[pi < p1 ? pi : p0];
+    const uint32_t o = 4u * (gi % (PAGE / 4));
+    m[q] = (pi < p1 && e.y > o) ? min(4u, e.y - o) : 0u;  // valid records of this group
+    x[q] = *reinterpret_cast<const uint4*>(pool + (size_t)e.x * PAGE + o);
   }
 #pragma unroll
-  for (uint32_t q = 0; q < KP; ++q) fn(x[q], m[q]);
+  for (int q = 0; q < IR; ++q) fn(x[q], m[q]);
 }
 
 // Direct half-tiles folded into their state rows: item = (half-bin, KP pages);
@@ -360,6 +385,40 @@ __global__ __launch_bounds__(WG) void k_pfold(const uint32_t* __restrict__ pool,
   }
 }
 
+// LDS counter add (RANK: returning the rank) where many lanes of the wave may share
+// a key (a hot tile of a super-tile; no plan names it here): twice, the first
+// pending lane's key is peeled off -- one atomic for all the lanes holding it, ranks
+// by mask_below -- and the remaining lanes add for themselves.  Convergent: every
+// lane calls it (valid = false: no record).
+template <bool RANK>
+__device__ __forceinline__ uint32_t peel_add(uint32_t* ctr, uint32_t key, bool valid) {
+  uint32_t rank = 0;
+  bool done = !valid;
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    const unsigned long long act = __ballot(!done);
+    if (!act) break;  // wave-uniform
+    const int leader = __ffsll((long long)act) - 1;
+    const uint32_t k0 = __builtin_amdgcn_readlane(key, leader);
+    const bool mine = !done && key == k0;
+    const unsigned long long m = __ballot(mine);
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(&ctr[k0], (uint32_t)__popcll(m));
+    if (RANK) base = __builtin_amdgcn_readlane(base, leader);
+    if (mine) {
+      rank = base + mask_below(m);
+      done = true;
+    }
+  }
+  if (!done) {
+    if (RANK)
+      rank = atomicAdd(&ctr[key], 1u);
+    else
+      atomicAdd(&ctr[key], 1u);
+  }
+  return rank;
+}
+
 // Level-2 item = (super-tile j, KP of its pages): records per tile of the super-tile.
 __global__ __launch_bounds__(WG) void k_p2count(const uint32_t* __restrict__ pool, const uint2* __restrict__ dir,
                                                 const uint32_t* __restrict__ pd, uint32_t F,
@@ -379,7 +438,7 @@ __global__ __launch_bounds__(WG) void k_p2count(const uint32_t* __restrict__ poo
       const uint32_t r[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if ((uint32_t)k < m) atomicAdd(&c[r[k] >> 26], 1u);
+        peel_add<false>(c, r[k] >> 26, (uint32_t)k < m);
     });
     __syncthreads();
     if (threadIdx.x < ST_TILES) cnt2[(size_t)item * ST_TILES + threadIdx.x] = c[threadIdx.x];
@@ -387,61 +446,61 @@ __global__ __launch_bounds__(WG) void k_p2count(const uint32_t* __restrict__ poo
   }
 }
 
-// Per super-tile (one 64-thread workgroup each): exclusive prefixes of its items'
-// tile counts (in place) and the tile totals.
-__global__ __launch_bounds__(64) void k_p2scan_a(const uint32_t* __restrict__ pd, uint32_t F,
-                                                 uint32_t* __restrict__ cnt2, uint32_t* __restrict__ tot) {
-  const uint32_t j = blockIdx.x, k = threadIdx.x;
+// Per super-tile (one 1024-thread workgroup each, lane = tile of the super-tile):
+// exclusive prefixes of its items' tile counts (in place) and the tile totals.  The
+// 16 waves take consecutive blocks of the items (a hot super-tile has thousands):
+// block sums, prefixes over the waves, then the in-place pass.
+__global__ __launch_bounds__(1024) void k_p2scan_a(const uint32_t* __restrict__ pd, uint32_t F,
+                                                   uint32_t* __restrict__ cnt2, uint32_t* __restrict__ tot) {
+  __shared__ uint32_t part[16][ST_TILES];
+  const uint32_t j = blockIdx.x, k = (uint32_t)lane_id(), w = threadIdx.x >> 6;
   const uint32_t i0 = pd[PD_LITEM + j], i1 = pd[PD_LITEM + j + 1];
-  uint32_t acc = 0;
+  const uint32_t n = i1 - i0, per = (n + 15) / 16;
+  const uint32_t a = i0 + min(n, w * per), b = i0 + min(n, (w + 1) * per);
   constexpr int U = 16;  // a batch of items' loads at once
-  for (uint32_t i = i0; i < i1; i += U) {
+  uint32_t acc = 0;
+  for (uint32_t i = a; i < b; i += U) {
     uint32_t v[U];
 #pragma unroll
-    for (int q = 0; q < U; ++q) v[q] = i + q < i1 ? cnt2[(size_t)(i + q) * ST_TILES + k] : 0u;
+    for (int q = 0; q < U; ++q) v[q] = i + q < b ? cnt2[(size_t)(i + q) * ST_TILES + k] : 0u;
+#pragma unroll
+    for (int q = 0; q < U; ++q) acc += v[q];
+  }
+  part[w][k] = acc;
+  __syncthreads();
+  uint32_t off = 0, all = 0;
+  for (uint32_t q = 0; q < 16; ++q) {
+    const uint32_t x = part[q][k];
+    off += q < w ? x : 0u;
+    all += x;
+  }
+  acc = off;
+  for (uint32_t i = a; i < b; i += U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) v[q] = i + q < b ? cnt2[(size_t)(i + q) * ST_TILES + k] : 0u;
 #pragma unroll
     for (int q = 0; q < U; ++q)
-      if (i + q < i1) {
+      if (i + q < b) {
         cnt2[(size_t)(i + q) * ST_TILES + k] = acc;
         acc += v[q];
       }
   }
   const uint32_t t = j * ST_TILES + k;
-  if (t < F) tot[t] = acc;
+  if (w == 0 && t < F) tot[t] = all;
 }
 
-// One workgroup: tile_base of the final layout (direct tiles hold no records in it),
-// and the next batch's direct tiles: the <= dmax biggest tiles of this batch (level-2
-// totals; a direct tile's from its half-bins) with >= max(thr_min, 2^k) records.
-__global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* __restrict__ pd,
-                                                   uint32_t* __restrict__ tot, uint32_t* __restrict__ plan,
-                                                   uint32_t* __restrict__ tile_base, uint32_t thr_min, uint32_t dmax) {
+// One workgroup: tile_base of the final layout (direct tiles hold no records in it).
+__global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* __restrict__ tot,
+                                                   uint32_t* __restrict__ tile_base) {
   __shared__ uint32_t lds[17];
-  __shared__ uint32_t lh[33];
-  __shared__ uint32_t sthr;
-  __shared__ uint4 lds4[17];
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t ND = plan[PLAN_ND];
   constexpr int PF = 32;  // F <= 32768 tiles: a thread's tiles [32 j, 32 j + 32)
   const uint32_t t0 = threadIdx.x * PF;
-  uint32_t v[PF], dirv[PF];
-  const uint32_t dbits = t0 < F ? plan[PLAN_DBITS + threadIdx.x] : 0u;
-  const uint32_t dpre = t0 < F ? plan[PLAN_DPRE + threadIdx.x] : 0u;
-#pragma unroll
-  for (int k = 0; k < PF; ++k) v[k] = t0 + k < F ? tot[t0 + k] : 0u;
-  if (threadIdx.x < 33) lh[threadIdx.x] = 0;
-  __syncthreads();
-  // this batch's totals: a direct tile's records are its two half-bins'
-  uint32_t s = 0;
+  uint32_t v[PF], s = 0;
 #pragma unroll
   for (int k = 0; k < PF; ++k) {
-    dirv[k] = v[k];
-    if ((dbits >> k) & 1u) {
-      const uint32_t d = dpre + (uint32_t)__popc(dbits & ((1u << k) - 1u));
-      dirv[k] = pd[PD_RECS + FS + 2 * d] + pd[PD_RECS + FS + 2 * d + 1];
-    }
+    v[k] = t0 + k < F ? tot[t0 + k] : 0u;
     s += v[k];
-    if (dmax > 0 && dirv[k] >= thr_min && dirv[k] > 0) atomicAdd(&lh[31 - __clz((int)dirv[k])], 1u);
   }
   uint32_t total;
   uint32_t acc = block_excl_scan<1024>(s, lds, &total);
@@ -451,8 +510,62 @@ __global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* _
       tile_base[t0 + k] = acc;
       acc += v[k];
     }
+  if (threadIdx.x == 0) tile_base[F] = total;
+}
+
+// This batch's direct tiles from a sample of its ids (before k_pbin1): PSAMPLE ids
+// at an even stride, counted per tile in LDS (u16 pairs) by PS_WG workgroups and
+// flushed with one global atomic per (workgroup, tile).  A direct tile only chooses
+// the path its records take, so an estimate is enough.
+constexpr uint32_t PSAMPLE = 1u << 20;
+constexpr int PS_WG = 64;
+__global__ __launch_bounds__(1024) void k_psample(const uint32_t* __restrict__ series, size_t n, uint32_t S,
+                                                  uint32_t F, uint32_t* __restrict__ pcount) {
+  __shared__ uint32_t c[16384];  // u16 pairs: tiles 2 i, 2 i + 1 (<= PSAMPLE / PS_WG = 16384 each)
+  for (uint32_t i = threadIdx.x; i < (F + 1) / 2; i += 1024) c[i] = 0;
+  __syncthreads();
+  const uint32_t per = PSAMPLE / PS_WG;
+  for (uint32_t k = threadIdx.x; k < per; k += 1024) {
+    const uint64_t i = (uint64_t)(blockIdx.x * per + k) * n / PSAMPLE;
+    const uint32_t s = series[i];
+    if (s < S) {
+      const uint32_t t = s >> TILE_SHIFT;
+      atomicAdd(&c[t >> 1], (t & 1u) ? 0x10000u : 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < (F + 1) / 2; i += 1024) {
+    const uint32_t x = c[i];
+    if (x & 0xFFFFu) atomicAdd(&pcount[2 * i], x & 0xFFFFu);
+    if ((x >> 16) && 2 * i + 1 < F) atomicAdd(&pcount[2 * i + 1], x >> 16);
+  }
+}
+
+// One workgroup: the direct set -- the <= dmax tiles with the biggest estimated
+// records (>= max(thr_min, 2^k), k the smallest power keeping <= dmax tiles).
+__global__ __launch_bounds__(1024) void k_pselect(uint32_t F, size_t n, uint32_t* __restrict__ pcount,
+                                                  uint32_t* __restrict__ plan, uint32_t thr_min, uint32_t dmax) {
+  __shared__ uint32_t lh[33];
+  __shared__ uint32_t sthr;
+  __shared__ uint4 lds4[17];
+  constexpr int PF = 32;
+  const uint32_t t0 = threadIdx.x * PF;
+  uint32_t est[PF];
+  if (threadIdx.x < 33) lh[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    uint32_t e = 0;
+    if (t0 + k < F) {
+      const uint32_t x = pcount[t0 + k];
+      if (x) pcount[t0 + k] = 0;  // ready for the next batch
+      e = (uint32_t)min((uint64_t)x * n / PSAMPLE, (uint64_t)0xFFFFFFFFu);  // each draw stands for n / PSAMPLE
+    }
+    est[k] = e;
+    if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    tile_base[F] = total;
     uint32_t cum = 0, thr = 0xFFFFFFFFu;
     int kbest = 32;
     if (dmax > 0)
@@ -465,15 +578,13 @@ __global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* _
     sthr = thr;
   }
   __syncthreads();
-  // the next batch's direct set: bitmap word j (tiles 32 j ..), prefix, list
   const uint32_t thr = sthr;
   uint32_t nb = 0;
 #pragma unroll
   for (int k = 0; k < PF; ++k)
-    if (t0 + k < F && dirv[k] >= thr) nb |= 1u << k;
+    if (t0 + k < F && est[k] >= thr) nb |= 1u << k;
   uint32_t cv[4] = {(uint32_t)__popc(nb), 0u, 0u, 0u}, ct[4];
   block_excl_scan4<1024>(cv, lds4, ct);
-  __syncthreads();  // every thread has read this batch's direct words (PLAN_DBITS / DPRE)
   if (t0 < F) {
     plan[PLAN_DBITS + threadIdx.x] = nb;
     plan[PLAN_DPRE + threadIdx.x] = cv[0];
@@ -487,12 +598,12 @@ __global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* _
     }
   }
   if (threadIdx.x == 0) plan[PLAN_ND] = ct[0];
-  (void)ND;
 }
 
 // Level 2: items re-read, 8K-record sub-chunks (two pages) LDS-sorted by tile and
 // written in sorted order to tile_base[t] + prefix(item, t) + running rank.
-constexpr int P2_CH = 2 * PAGE;
+constexpr int P2_CH = 8192;  // records per sub-chunk: P2_CH / PAGE pages
+static_assert(P2_CH % PAGE == 0, "whole pages per sub-chunk");
 constexpr int P2_NT = 512;
 __global__ __launch_bounds__(P2_NT) void k_p2place(const uint32_t* __restrict__ pool, const uint2* __restrict__ dir,
                                                    const uint32_t* __restrict__ pd, uint32_t F,
@@ -511,39 +622,35 @@ __global__ __launch_bounds__(P2_NT) void k_p2place(const uint32_t* __restrict__ 
   for (uint32_t i = threadIdx.x; i <= FS; i += P2_NT) ib[i] = pd[PD_LITEM + i];
   __syncthreads();
   for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-    const uint32_t j = upper_index(ib, FS, item);
-    const uint32_t p0 = pd[PD_BASE + j] + (item - ib[j]) * KP;
-    const uint32_t p1 = min(p0 + KP, pd[PD_BASE + j + 1]);
+    const uint32_t j = __builtin_amdgcn_readfirstlane(upper_index(ib, FS, item));
+    const uint32_t p0 = __builtin_amdgcn_readfirstlane(pd[PD_BASE + j] + (item - ib[j]) * KP);
+    const uint32_t p1 = __builtin_amdgcn_readfirstlane(min(p0 + KP, pd[PD_BASE + j + 1]));
     if (threadIdx.x < ST_TILES) {
       const uint32_t t = j * ST_TILES + threadIdx.x;
       cnt[threadIdx.x] = 0;
       cur[threadIdx.x] = t < F ? tile_base[t] + pre2[(size_t)item * ST_TILES + threadIdx.x] : 0u;
     }
     __syncthreads();
-    for (uint32_t pp = p0; pp < p1; pp += 2) {
-      // this thread's records: 16-B groups of the (up to) two pages
+    for (uint32_t pp = p0; pp < p1; pp += P2_CH / PAGE) {
+      // this thread's records: 16-B groups of the sub-chunk's pages
       constexpr int G4 = P2_CH / 4 / P2_NT;  // 4 groups per thread
       uint4 x[G4];
       uint32_t m[G4];
 #pragma unroll
-      for (int q = 0; q < G4; ++q) {
+      for (int q = 0; q < G4; ++q) {  // branch-free, all loads issued at once (as item_records)
         const uint32_t gi = (uint32_t)q * P2_NT + threadIdx.x;  // group in the sub-chunk
         const uint32_t page = pp + gi / (PAGE / 4);
         const uint32_t o = 4u * (gi % (PAGE / 4));
-        m[q] = 0;
-        x[q] = make_uint4(0u, 0u, 0u, 0u);
-        if (page < p1) {
-          const uint2 e = dir[page];
-          m[q] = e.y > o ? min(4u, e.y - o) : 0u;
-          if (m[q]) x[q] = *reinterpret_cast<const uint4*>(pool + (size_t)e.x * PAGE + o);
-        }
+        const uint2 e = dir[page < p1 ? page : p0];
+        m[q] = (page < p1 && e.y > o) ? min(4u, e.y - o) : 0u;
+        x[q] = *reinterpret_cast<const uint4*>(pool + (size_t)e.x * PAGE + o);
       }
       uint32_t rk[4 * G4];
 #pragma unroll
       for (int q = 0; q < G4; ++q) {
         const uint32_t r[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) rk[4 * q + k] = (uint32_t)k < m[q] ? atomicAdd(&cnt[r[k] >> 26], 1u) : 0u;
+        for (int k = 0; k < 4; ++k) rk[4 * q + k] = peel_add<true>(cnt, r[k] >> 26, (uint32_t)k < m[q]);
       }
       __syncthreads();
       if (threadIdx.x < 64) {
@@ -602,7 +709,9 @@ hipError_t launch_paged_ingest(const PagedArgs& a, int phase, hipStream_t st) {
   const uint32_t FS = (a.F + ST_TILES - 1) / ST_TILES;
   hipError_t e = hipSuccess;
   switch (phase) {
-    case 0:  // level 1 into the page pools
+    case 0:  // this batch's direct tiles (a sample), then level 1 into the page pools
+      hipLaunchKernelGGL(k_psample, dim3(PS_WG), dim3(1024), 0, st, a.series, a.n, a.S, a.F, a.pcount);
+      hipLaunchKernelGGL(k_pselect, dim3(1), dim3(1024), 0, st, a.F, a.n, a.pcount, a.plan, a.thr_min, a.dmax);
       hipLaunchKernelGGL((k_pbin1<16384, 1024>), dim3(a.G), dim3(1024), pbin1_lds(16384), st, a.series, a.values, a.n,
                          a.per, a.S, a.F, a.plan, a.tb, a.state.sumfix, a.err, a.pool_pages, a.pool, a.plog, a.nlog,
                          a.tailpg, a.vec ? 1 : 0);
@@ -621,9 +730,8 @@ hipError_t launch_paged_ingest(const PagedArgs& a, int phase, hipStream_t st) {
       break;
     default:  // level 2 of the other tiles into the final layout; the next batch's direct set
       hipLaunchKernelGGL(k_p2count, dim3(2 * ncu), dim3(WG), 0, st, a.pool, a.dir, a.pd, a.F, a.cnt2);
-      hipLaunchKernelGGL(k_p2scan_a, dim3(FS), dim3(64), 0, st, a.pd, a.F, a.cnt2, a.tot);
-      hipLaunchKernelGGL(k_p2scan_b, dim3(1), dim3(1024), 0, st, a.F, a.pd, a.tot, a.plan, a.tile_base, a.thr_min,
-                         a.dmax);
+      hipLaunchKernelGGL(k_p2scan_a, dim3(FS), dim3(1024), 0, st, a.pd, a.F, a.cnt2, a.tot);
+      hipLaunchKernelGGL(k_p2scan_b, dim3(1), dim3(1024), 0, st, a.F, a.tot, a.tile_base);
       hipLaunchKernelGGL(k_p2place, dim3(4 * ncu), dim3(P2_NT), P2PLACE_LDS, st, a.pool, a.dir, a.pd, a.F, a.cnt2,
                          a.tile_base, a.records);
       break;
