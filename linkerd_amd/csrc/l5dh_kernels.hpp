@@ -185,7 +185,8 @@ hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* d
 // tiles counted and placed from a page directory.  Items = KP pages.
 constexpr int PG_BINS = BIN1_BINS;
 constexpr uint32_t PAGE = 1024;  // records per page (4 KB): a cold bin's slab run fills most of one
-constexpr uint32_t KP = 32;     // pages per item (32K records)
+constexpr uint32_t KP = 32;     // pages per level-2 item (32K records)
+constexpr uint32_t KPD = 256;   // pages per direct-fold item (2^18 records)
 constexpr int PD_WORDS = 5136;  // per-bin page / record counts, bases, item bases, header
 constexpr size_t PFOLD_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + LUT2_N * 8 + (2 * DIRECT_MAX + 2) * 4;
 constexpr size_t P2PLACE_LDS = (size_t)8192 * 8 + 3 * 64 * 4 + 513 * 4;

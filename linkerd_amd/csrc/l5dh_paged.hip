@@ -208,8 +208,8 @@ __global__ __launch_bounds__(256) void k_pdir_count(const uint2* __restrict__ pl
   }
 }
 
-// One workgroup: page bases per bin, items of KP pages per direct half-bin and per
-// super-tile (the trash bin has none).
+// One workgroup: page bases per bin, items of KPD pages per direct half-bin and of
+// KP pages per super-tile (the trash bin has none).
 __global__ __launch_bounds__(1024) void k_pdir_scan(uint32_t F, const uint32_t* __restrict__ plan,
                                                     uint32_t* __restrict__ pd) {
   __shared__ uint4 lds4[17];
@@ -217,8 +217,8 @@ __global__ __launch_bounds__(1024) void k_pdir_scan(uint32_t F, const uint32_t* 
   const uint32_t ND = plan[PLAN_ND];
   const uint32_t b = threadIdx.x;  // PG_BINS == 1024
   const uint32_t np = pd[PD_PAGES + b];
-  const uint32_t ni = (np + KP - 1) / KP;
-  uint32_t v[4] = {np, (b >= FS && b < FS + 2 * ND) ? ni : 0u, b < FS ? ni : 0u, 0u}, tot[4];
+  uint32_t v[4] = {np, (b >= FS && b < FS + 2 * ND) ? (np + KPD - 1) / KPD : 0u, b < FS ? (np + KP - 1) / KP : 0u, 0u},
+           tot[4];
   block_excl_scan4<1024>(v, lds4, tot);
   pd[PD_BASE + b] = v[0];
   pd[PD_CUR + b] = 0;
@@ -326,7 +326,7 @@ __device__ __forceinline__ void item_records(const uint32_t* __restrict__ pool, 
   for (int q = 0; q < IR; ++q) fn(x[q], m[q]);
 }
 
-// Direct half-tiles folded into their state rows: item = (half-bin, KP pages);
+// Direct half-tiles folded into their state rows: item = (half-bin, KPD pages);
 // u32 LDS bins of the half's 16 series, lane-private u64 value sums, flushed with
 // global atomics (k_pdir_init prepared the rows).  Persistent.
 __global__ __launch_bounds__(WG) void k_pfold(const uint32_t* __restrict__ pool, const uint2* __restrict__ dir,
@@ -351,9 +351,11 @@ __global__ __launch_bounds__(WG) void k_pfold(const uint32_t* __restrict__ pool,
     __syncthreads();
     const uint32_t h = upper_index(ib, 2 * ND, item);  // half-bin h = 2 d + half
     const uint32_t b = FS + h;
-    const uint32_t p0 = pd[PD_BASE + b] + (item - ib[h]) * KP;
-    const uint32_t p1 = min(p0 + KP, pd[PD_BASE + b + 1]);
-    item_records(pool, dir, p0, p1, [&](uint4 x, uint32_t m) {
+    const uint32_t p0 = pd[PD_BASE + b] + (item - ib[h]) * KPD;
+    const uint32_t p1 = min(p0 + KPD, pd[PD_BASE + b + 1]);
+    // (a direct item is KPD / KP batches of pages: the LDS clear and the 16-row
+    // global flush are paid per 2^18 records, as k_accum_split's items)
+    for (uint32_t pb = p0; pb < p1; pb += KP) item_records(pool, dir, pb, min(pb + KP, p1), [&](uint4 x, uint32_t m) {
       const uint32_t r[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
