@@ -31,7 +31,7 @@ constexpr int ST_TILES = 64;
 constexpr int ST_SHIFT = 11;
 
 // payload of a sample outside [0, V_ESC): exact contribution to sumfix, V_ESC + bucket
-__device__ __noinline__ uint32_t ppayload_slow(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
+__device__ __forceinline__ uint32_t ppayload_slow(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
   int64_t c;
   const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
   if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;
@@ -104,22 +104,40 @@ __global__ __launch_bounds__(NT, 1) void k_pbin1(const uint32_t* __restrict__ se
         if (!in) inm &= ~(1u << k);
       }
     }
+    // payloads: +0 <= f < V_ESC by one compare of the bit pattern; the rare rest exactly,
+    // from a non-unrolled loop over this thread's escaped slots staged in its own part
+    // of the (still free) stage -- one inlined copy of the full search
     uint32_t rec[PT], pk[PT];
+    uint32_t escm = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t s = sv[k];
-      const float f = fv[k];
       const bool ok = s < S;
       bad |= !ok && ((inm >> k) & 1u);
-      // fast: +0 <= f < V_ESC by one compare of the bit pattern; the rest exactly
-      uint32_t pl = __float_as_uint(f) < 0x49FFC000u ? (uint32_t)f : 0u;
-      if (ok && __float_as_uint(f) >= 0x49FFC000u) pl = ppayload_slow(s, f, tb, sumfix);
+      const bool fast = __float_as_uint(fv[k]) < 0x49FFC000u;
+      escm |= (ok && !fast) ? (1u << k) : 0u;
+      rec[k] = ((s & (ST_TILES * TILE - 1)) << 21) | (fast ? (uint32_t)fv[k] : 0u);
+    }
+    if (__ballot(escm != 0u)) {
+      uint2* tmp = stage + threadIdx.x * PT;
+#pragma unroll
+      for (int k = 0; k < PT; ++k) tmp[k] = make_uint2(sv[k], __float_as_uint(fv[k]));
+#pragma unroll 1
+      for (int k = 0; k < PT; ++k)
+        if ((escm >> k) & 1u) tmp[k].x = ppayload_slow(tmp[k].x, __uint_as_float(tmp[k].y), tb, sumfix);
+#pragma unroll
+      for (int k = 0; k < PT; ++k)
+        if ((escm >> k) & 1u) rec[k] = ((sv[k] & (ST_TILES * TILE - 1)) << 21) | tmp[k].x;
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t s = sv[k];
+      const bool ok = s < S;
       const uint2 d = dw[(s >> (TILE_SHIFT + 5)) & 1023u];
       const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);
       const bool direct = __builtin_amdgcn_ubfe(d.x, tw, 1) != 0u;
       const uint32_t dbin = FS + 2u * (d.y + (uint32_t)__popc(__builtin_amdgcn_ubfe(d.x, 0, tw))) + ((s >> 4) & 1u);
       const uint32_t b = sel_u32(ok, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
-      rec[k] = ((s & (ST_TILES * TILE - 1)) << 21) | pl;
       pk[k] = atomicAdd(cnt + b, 1u) | (b << 14);
     }
     __syncthreads();
@@ -633,13 +651,12 @@ __global__ __launch_bounds__(P2_NT) void k_p2place(const uint32_t* __restrict__ 
       cur[threadIdx.x] = t < F ? tile_base[t] + pre2[(size_t)item * ST_TILES + threadIdx.x] : 0u;
     }
     __syncthreads();
-    for (uint32_t pp = p0; pp < p1; pp += P2_CH / PAGE) {
-      // this thread's records: 16-B groups of the sub-chunk's pages
-      constexpr int G4 = P2_CH / 4 / P2_NT;  // 4 groups per thread
-      uint4 x[G4];
-      uint32_t m[G4];
+    // this thread's records: 16-B groups of a sub-chunk's pages, branch-free, all loads
+    // issued at once; the next sub-chunk's are in flight while this one is sorted
+    constexpr int G4 = P2_CH / 4 / P2_NT;  // 4 groups per thread
+    auto load = [&](uint32_t pp, uint4 (&x)[G4], uint32_t (&m)[G4]) {
 #pragma unroll
-      for (int q = 0; q < G4; ++q) {  // branch-free, all loads issued at once (as item_records)
+      for (int q = 0; q < G4; ++q) {
         const uint32_t gi = (uint32_t)q * P2_NT + threadIdx.x;  // group in the sub-chunk
         const uint32_t page = pp + gi / (PAGE / 4);
         const uint32_t o = 4u * (gi % (PAGE / 4));
@@ -647,6 +664,19 @@ __global__ __launch_bounds__(P2_NT) void k_p2place(const uint32_t* __restrict__ 
         m[q] = (page < p1 && e.y > o) ? min(4u, e.y - o) : 0u;
         x[q] = *reinterpret_cast<const uint4*>(pool + (size_t)e.x * PAGE + o);
       }
+    };
+    uint4 xn[G4];
+    uint32_t mn[G4];
+    load(p0, xn, mn);
+    for (uint32_t pp = p0; pp < p1; pp += P2_CH / PAGE) {
+      uint4 x[G4];
+      uint32_t m[G4];
+#pragma unroll
+      for (int q = 0; q < G4; ++q) {
+        x[q] = xn[q];
+        m[q] = mn[q];
+      }
+      if (pp + P2_CH / PAGE < p1) load(pp + P2_CH / PAGE, xn, mn);
       uint32_t rk[4 * G4];
 #pragma unroll
       for (int q = 0; q < G4; ++q) {
