@@ -67,7 +67,7 @@ enum {
   L5DH_PARAM_COLD_LIMIT = 2,  /* max records for the single-pass tile path (<= 65535) */
   L5DH_PARAM_HOT_CHUNK = 3,   /* max records per work item on the big-tile paths, 1024..2^20 (fewer when CUs would idle) */
   L5DH_PARAM_MAX_SEGMENTS = 4, /* binned ingest batches kept before folding (1..8) */
-  L5DH_PARAM_BIN_MODE = 5,     /* 0 auto, 1 single-level scatter, 2 two-level partition */
+  L5DH_PARAM_BIN_MODE = 5,     /* 0 auto (= 2), 1 single-level scatter, 2 two-level partition, 3 paged two-level (no counting pass) */
   L5DH_PARAM_DIRECT_MAX = 6,   /* tiles whose final records k_bin1 writes directly (0..255) */
   L5DH_PARAM_DIRECT_DIV = 7,   /* direct tiles average >= 1/div records per 8K-sample sub-chunk */
   L5DH_PARAM_SPLIT_MIN = 8,    /* tiles laid out per half-tile have >= this many records per batch */
