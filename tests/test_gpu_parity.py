@@ -192,14 +192,15 @@ def test_split_tiles_across_batches(oracle, direct_max, mode):
 
 
 @pytest.mark.parametrize("value", [5.0, 2_000_000.0])
-def test_split_bins_one_bucket(oracle, value):
+@TWO_LEVEL
+def test_split_bins_one_bucket(oracle, value, mode):
     """A split half-tile whose 300k records per batch all fall in ONE bucket: one LDS
     bin of a 2^18-record split item reaches 2^18 (u32 bins), the dense state row
     accumulates across batches.  At 2e6 (the largest payloads below the escape) one
     lane's value-sum slot of an item takes 4096 x 2e6 > 2^32 (u64 slots)."""
     rng = np.random.default_rng(5)
     S = 64
-    eng = _engine(S, 2)
+    eng = _engine(S, mode)
     eng.set_param(N.PARAM_SPLIT_MIN, 1000)
     o = oracle.OracleHistograms(S)
     for it in range(3):  # the first batch makes tile 0 split for the later ones
@@ -260,11 +261,12 @@ def test_big_tile_bins_past_u16(oracle, mode):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"big tile {it}")
 
 
-def test_range_snapshot_peek_export(oracle):
+@TWO_LEVEL
+def test_range_snapshot_peek_export(oracle, mode):
     rng = np.random.default_rng(21)
     S = 500
     series, vals = _random_batch(rng, S, 100_000)
-    eng = _engine(S)
+    eng = _engine(S, mode)
     eng.ingest(series, vals)
     o = oracle.OracleHistograms(S)
     o.ingest(series, vals)
@@ -297,9 +299,10 @@ def test_range_snapshot_peek_export(oracle):
     _assert_summaries_equal(summ, want_after, "summarize_dense")
 
 
-def test_invalid_series_reported(oracle):
+@TWO_LEVEL
+def test_invalid_series_reported(oracle, mode):
     S = 64
-    eng = _engine(S)
+    eng = _engine(S, mode)
     series = np.array([1, 2, 64, 3, 1000], dtype=np.uint32)
     vals = np.array([1, 2, 3, 4, 5], dtype=np.float32)
     with pytest.raises(N.L5dhError):  # detected by the kernels; reported by ingest or at the latest by sync
@@ -325,12 +328,13 @@ def test_c2_slice_bitexact(oracle, bin_mode):
     _assert_summaries_equal(got, o.snapshot(), "c2 slice")
 
 
-def test_device_buffers_in_and_out(oracle):
+@TWO_LEVEL
+def test_device_buffers_in_and_out(oracle, mode):
     import torch
     rng = np.random.default_rng(4)
     S = 2000
     series, vals = _random_batch(rng, S, 500_000)
-    eng = _engine(S)
+    eng = _engine(S, mode)
     ds = torch.from_numpy(series.view(np.int32)).cuda()
     dv = torch.from_numpy(vals).cuda()
     eng.ingest(ds, dv)
