@@ -164,6 +164,9 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
                                                  uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
   __shared__ uint4 lds4[17];
   __shared__ uint32_t base[4];
+  __shared__ uint32_t nbig;
+  __shared__ uint4 big[64];  // {tile | split << 31, first item, half-0 records, records}
+  if (threadIdx.x == 0) nbig = 0;  // (visible after the scans' barriers)
   const uint32_t B = gridDim.x;
   // workgroup bases: the earlier workgroups' counts (B <= 1024: a thread per workgroup),
   // summed by one reduction; workgroup 0 also writes the header totals
@@ -198,23 +201,50 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   const uint32_t xa = base[1] + pv[1];
   uint32_t ha = base[2] + pv[2];
   uint32_t sa = base[3] + pv[3];
-  if (t >= F) return;
-  uint8_t flags = dirty[t] ? TF_DIRTY : 0;
-  if (c.hot) {
-    if (c.h0 != 0xFFFFFFFFu) {
-      flags |= TF_SPLIT;
-      for (uint32_t h = 0; h < 2; ++h) {
-        const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
-        for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
+  // a tile with many chunk items (C3's tile 0: ~1000) has them written by the whole
+  // workgroup below, not by its one thread
+  bool coop = false;
+  if (t < F && c.hot && c.si + c.hi > 32) {
+    const uint32_t k = atomicAdd(&nbig, 1u);
+    if (k < 64) {
+      big[k] = make_uint4(t | (c.h0 != 0xFFFFFFFFu ? 0x80000000u : 0u), c.h0 != 0xFFFFFFFFu ? sa : ha, c.h0, tot);
+      coop = true;
+    }
+  }
+  if (t < F) {
+    uint8_t flags = dirty[t] ? TF_DIRTY : 0;
+    if (c.hot) {
+      if (c.h0 != 0xFFFFFFFFu) {
+        flags |= TF_SPLIT;
+        for (uint32_t h = 0; !coop && h < 2; ++h) {
+          const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
+          for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
+        }
+      } else if (!coop) {
+        for (uint32_t q = 0; q < c.hi; ++q) plan.hot_item[ha + q] = t | (q << 15);
+      }
+      plan.hot_list[xa] = t;
+    } else if (c.ci) {
+      plan.cold_tile[ca] = t;
+    }
+    plan.tile_flags[t] = flags;
+  }
+  __syncthreads();
+  const uint32_t nb = min(nbig, 64u);
+  for (uint32_t k = 0; k < nb; ++k) {
+    const uint4 e = big[k];
+    const uint32_t tt = e.x & 0x7FFFFFFFu;
+    if (e.x >> 31) {  // split: half 0's chunks, then half 1's
+      const uint32_t n0 = (e.z + hot_chunk - 1) / hot_chunk, n1 = (e.w - e.z + hot_chunk - 1) / hot_chunk;
+      for (uint32_t i = threadIdx.x; i < n0 + n1; i += 1024) {
+        const uint32_t h = i >= n0 ? 1u : 0u;
+        plan.split_item[e.y + i] = make_uint2(tt | (h << 15), h ? i - n0 : i);
       }
     } else {
-      for (uint32_t q = 0; q < c.hi; ++q) plan.hot_item[ha + q] = t | (q << 15);
+      const uint32_t n = (e.w + hot_chunk - 1) / hot_chunk;
+      for (uint32_t i = threadIdx.x; i < n; i += 1024) plan.hot_item[e.y + i] = tt | (i << 15);
     }
-    plan.hot_list[xa] = t;
-  } else if (c.ci) {
-    plan.cold_tile[ca] = t;
   }
-  plan.tile_flags[t] = flags;
 }
 
 // k_hot_init: split tiles accumulate with global atomics into state rows, so
