@@ -140,7 +140,10 @@ int l5dh_ingest_wait(l5dh_ctx* ctx, uint64_t ticket);
  * batched over series [first, first+count).  out (nullable) receives one
  * l5dh_summary per series (Metric.scala:53-67); counts_out (nullable)
  * receives [count][1798] int32 bucket counts (what reset()/peek return, dense).
- * reset != 0 clears those series afterwards, atomically with the snapshot. */
+ * reset != 0 clears those series afterwards, atomically with the snapshot.
+ * The call returns once the outputs are written, except when every output given
+ * is device memory and the context runs on a caller stream (l5dh_set_stream):
+ * then the outputs are stream ordered on that stream (no host wait). */
 int l5dh_snapshot(l5dh_ctx* ctx, uint32_t first, uint32_t count, l5dh_summary* out,
                   int32_t* counts_out, int reset);
 

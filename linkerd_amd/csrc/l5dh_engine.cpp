@@ -731,6 +731,9 @@ int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, 
     if (counts_out && !cnt_dev)
       HIPCHK(c, hipMemcpyAsync(counts_out, d_counts, (size_t)count * NB * 4, hipMemcpyDefault, c->stream));
   }
+  // device outputs on a caller stream are stream ordered (as device inputs of
+  // l5dh_ingest): the caller's later work on that stream sees them; no host wait
+  if ((!out || out_dev) && (!counts_out || cnt_dev) && c->stream != c->own_stream) return 0;
   return sync_stream(c);
 }
 
