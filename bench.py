@@ -61,12 +61,12 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # (COST_PS_PER_SAMPLE per Zipf-expected sample + COST_PS_PER_SERIES per series row)
 # times a measured correction per Zipf-rank range -- each range's measured shard
 # time over its base-model time, from the 8 single-GPU runs of `--shard r/8`
-# (the sweep profiles/r02l_shards_before.jsonl; profiles/r02l_shards.jsonl is this calibration's result): direct
+# (the sweep profiles/r02q_shards_before.jsonl, after the stream-ordered snapshot): direct
 # tiles, split tiles through level 2 and cold tiles cost differently per sample
 COST_PS_PER_SAMPLE = 6.5
 COST_PS_PER_SERIES = 1700.0
-COST_CALIBRATION = ((0, 1.0951), (8, 1.0959), (113, 1.1246), (1690, 1.2387), (14169, 1.1297), (68007, 1.1774),
-                    (260166, 1.1677), (589995, 1.1323))  # (first Zipf rank, ms of that r/8 shard)
+COST_CALIBRATION = ((0, 1.113), (9, 1.0976), (144, 1.2229), (2083, 1.1024), (14736, 1.1316), (72077, 1.1337),
+                    (262409, 1.1106), (585838, 1.1252))  # (first Zipf rank, ms of that r/8 shard)
 
 
 def parse():
