@@ -226,6 +226,39 @@ def _stream_ordered_body(oracle, torch, HistogramEngine):
     eng.close()
 
 
+@pytest.mark.parametrize("mode", [2, 3], ids=["twolevel", "paged"])
+def test_snapshot_stream_ordered_on_caller_stream(oracle, mode):
+    """An engine on torch's stream (l5dh_set_stream) with device outputs returns from
+    l5dh_snapshot without a host wait: batches generated, ingested and snapshotted
+    back to back, each snapshot read by torch work queued behind it, no synchronize
+    in between -- every interval bit-exact (reset: each holds only its own batch)."""
+    import torch
+    from linkerd_amd.engine import HistogramEngine
+    S = 3000
+    dev = torch.device("cuda", 0)
+    with torch.cuda.stream(torch.cuda.Stream()):
+        eng = HistogramEngine(S)
+        eng.set_param(N.PARAM_BIN_MODE, mode)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        batches = [synth.c3(S=S, N=400_000, seed=90 + k) for k in range(4)]
+        dbat = [(torch.from_numpy(sr.astype(np.int32)).to(dev), torch.from_numpy(v).to(dev)) for sr, v in batches]
+        torch.cuda.synchronize()
+        outs = []
+        for ds, dv in dbat:
+            eng.ingest(ds, dv)
+            summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
+            counts = torch.empty((S, N.NBUCKETS), dtype=torch.int32, device=dev)
+            eng.snapshot_into(summ, counts, reset=True)
+            outs.append((summ.clone(), counts.sum(dim=0)))  # torch work behind the snapshot
+        torch.cuda.synchronize()
+        for (sr, v), (summ, csum) in zip(batches, outs):
+            o = oracle.OracleHistograms(S)
+            o.ingest(sr, v)
+            np.testing.assert_array_equal(csum.cpu().numpy(), o.counts().sum(axis=0))
+            _eq_summaries(summ.cpu().numpy().view(N.SUMMARY_DTYPE).reshape(-1), o.snapshot())
+        eng.close()
+
+
 def test_concurrent_adds_and_snapshots_bitexact(oracle):
     """8 producer threads (Stat.add through per-thread staging, and direct batched
     ingest) while a timer thread snapshots with reset: the snapshots together hold
