@@ -531,6 +531,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     a.cnt2 = static_cast<uint32_t*>(c->cnt2.p);
     a.tot = c->d_ptot;
     a.pcount = c->d_pcount;
+    a.err_host = c->h_header_dev + 4;
     a.tile_base = sg.tbase;
     a.records = static_cast<uint32_t*>(sg.recs.p);
     a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
@@ -555,8 +556,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     }
     sg.n = n;
     c->nseg++;
-    HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-    return 0;
+    return 0;  // (k_p2scan_b wrote the invalid-id count to h_header[4])
   }
   const bool two_level = c->bin_mode != 1;
   // split set of this batch (chosen from the previous batch's tile totals) and of the next
@@ -585,7 +585,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
                               // the hot k_bin1 bins (ballot ranking when one holds >= half); all 8
                               // for the lane-private-slot development variant (L5DH_DBG bit 22)
                               1 | (((c->dbg >> 22) & 1) ? 4 : 0),
-                              c->stream));
+                              c->d_err, c->h_header_dev + 4, c->stream));
       c->split_cur ^= 1;
     }
     {
@@ -604,8 +604,9 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   }
   sg.n = n;
   c->nseg++;
-  // the invalid-id counter follows the batch to the host asynchronously (check_err)
-  HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+  // the invalid-id counter follows the batch to the host asynchronously (check_err):
+  // k_stplan writes it to the mapped pinned word; the single-level path copies it
+  if (!two_level) HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
   return 0;
 }
 

@@ -637,7 +637,10 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
 __global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
                                                  uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
                                                  uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax,
-                                                 uint32_t split_min, int hot_bins) {
+                                                 uint32_t split_min, int hot_bins, const uint32_t* __restrict__ err,
+                                                 uint32_t* __restrict__ err_host) {
+  // the invalid-id count of k_count, to the host's mapped pinned word (no copy launch)
+  if (threadIdx.x == 0) *reinterpret_cast<volatile uint32_t*>(err_host) = *err;
   __shared__ uint4 lds4[17];
   __shared__ unsigned long long best[16];
   __shared__ uint32_t lhd[33], lhs[33];
@@ -1122,11 +1125,11 @@ hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, siz
 
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
                          uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, int hot_bins,
-                         hipStream_t st) {
+                         const uint32_t* err, uint32_t* err_host, hipStream_t st) {
   const uint32_t FS = (F + 63) / 64;
   const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
   hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap),
-                     split_min, hot_bins);
+                     split_min, hot_bins, err, err_host);
   return hipGetLastError();
 }
 

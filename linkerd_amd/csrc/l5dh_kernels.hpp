@@ -150,7 +150,7 @@ constexpr int PLAN_WORDS = PLAN_ITEMS + PLAN_ITEMS_MAX / 2;
 // `nxt`: the tiles with records >= max(split_min, 2^k) (<= SPLIT_MAX tiles).
 hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
                          uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, int hot_bins,
-                         hipStream_t st);
+                         const uint32_t* err, uint32_t* err_host, hipStream_t st);
 hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                        uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
                        const uint32_t* coltot, const uint32_t* split, uint32_t* scratch1, uint32_t* records,
@@ -210,6 +210,7 @@ struct PagedArgs {
   uint32_t* cnt2;        // [level-2 items * 64]
   uint32_t* tot;         // [F] tile totals of the final layout
   uint32_t* pcount;      // [F] sampled ids per tile (zero between batches)
+  uint32_t* err_host;    // mapped pinned word: the invalid-id count, written after level 1
   uint32_t* tile_base;   // [F + 1] the segment's tile offsets
   uint32_t* records;     // the segment's final layout
   uint32_t thr_min, dmax;

@@ -512,7 +512,10 @@ __global__ __launch_bounds__(1024) void k_p2scan_a(const uint32_t* __restrict__ 
 
 // One workgroup: tile_base of the final layout (direct tiles hold no records in it).
 __global__ __launch_bounds__(1024) void k_p2scan_b(uint32_t F, const uint32_t* __restrict__ tot,
-                                                   uint32_t* __restrict__ tile_base) {
+                                                   uint32_t* __restrict__ tile_base, const uint32_t* __restrict__ err,
+                                                   uint32_t* __restrict__ err_host) {
+  // k_pbin1's invalid-id count, to the host's mapped pinned word (no copy launch)
+  if (threadIdx.x == 0) *reinterpret_cast<volatile uint32_t*>(err_host) = *err;
   __shared__ uint32_t lds[17];
   constexpr int PF = 32;  // F <= 32768 tiles: a thread's tiles [32 j, 32 j + 32)
   const uint32_t t0 = threadIdx.x * PF;
@@ -763,7 +766,7 @@ hipError_t launch_paged_ingest(const PagedArgs& a, int phase, hipStream_t st) {
     default:  // level 2 of the other tiles into the final layout; the next batch's direct set
       hipLaunchKernelGGL(k_p2count, dim3(2 * ncu), dim3(WG), 0, st, a.pool, a.dir, a.pd, a.F, a.cnt2);
       hipLaunchKernelGGL(k_p2scan_a, dim3(FS), dim3(1024), 0, st, a.pd, a.F, a.cnt2, a.tot);
-      hipLaunchKernelGGL(k_p2scan_b, dim3(1), dim3(1024), 0, st, a.F, a.tot, a.tile_base);
+      hipLaunchKernelGGL(k_p2scan_b, dim3(1), dim3(1024), 0, st, a.F, a.tot, a.tile_base, a.err, a.err_host);
       hipLaunchKernelGGL(k_p2place, dim3(4 * ncu), dim3(P2_NT), P2PLACE_LDS, st, a.pool, a.dir, a.pd, a.F, a.cnt2,
                          a.tile_base, a.records);
       break;
