@@ -571,8 +571,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_colscan(c->d_table, G, c->F, c->d_tile_tot, c->stream));
-    HIPCHK(c, launch_tilescan(c->d_tile_tot, c->F, cur, sg.tbase, c->stream));
-    HIPCHK(c, launch_seginfo(cur, c->d_tile_tot, c->F, sg.sinfo, c->stream));
+    HIPCHK(c, launch_tilescan_seg(c->d_tile_tot, c->F, cur, sg.tbase, sg.sinfo, c->stream));
   }
   if (two_level) {
     int r = ensure(c, c->scratch1, (n + BIN1_SCRATCH_PAD) * 4);  // trash bin; k_bin2 reads whole 16-B groups

@@ -249,6 +249,57 @@ __global__ __launch_bounds__(1024) void k_tilescan(uint32_t* __restrict__ coltot
   }
   if (threadIdx.x == 0) tile_base[F] = tot;
 }
+// k_tilescan + k_seginfo in one workgroup, through LDS: the column totals are loaded
+// coalesced (a thread's 32 consecutive tiles read strided from global memory were
+// ~30 us on C3), split tiles add their halves, every thread scans its 32 consecutive
+// tiles from LDS (one pad word per 32: no bank conflicts), and tile_base goes out
+// coalesced.  F <= 32768.
+constexpr uint32_t tpad(uint32_t t) { return t + (t >> 5); }
+__global__ __launch_bounds__(1024) void k_tilescan_seg(uint32_t* __restrict__ coltot, uint32_t F,
+                                                       const uint32_t* __restrict__ split,
+                                                       uint32_t* __restrict__ tile_base, uint32_t* __restrict__ sinfo) {
+  extern __shared__ uint32_t tl[];  // [tpad(F) + 1]
+  __shared__ uint32_t lds[17];
+  const uint32_t NS = split[0];
+  uint16_t* map = reinterpret_cast<uint16_t*>(sinfo + SINFO_MAP);
+  for (uint32_t t = threadIdx.x; t < F; t += 1024) {
+    tl[tpad(t)] = coltot[t];
+    map[t] = NO_SPLIT;
+  }
+  __syncthreads();
+  // split tiles: their samples were counted in the two half columns
+  for (uint32_t si = threadIdx.x; si < NS; si += 1024) {
+    const uint32_t t = split[SPLIT_LIST + si];
+    const uint32_t h0 = coltot[F + 2 * si], h1 = coltot[F + 2 * si + 1];
+    const uint32_t v = tl[tpad(t)] + h0 + h1;
+    tl[tpad(t)] = v;
+    coltot[t] = v;  // read as the tile's total by k_stplan
+    sinfo[1 + si] = t;
+    sinfo[SINFO_H0 + si] = h0;
+    map[t] = (uint16_t)si;
+  }
+  if (threadIdx.x == 0) sinfo[0] = NS;
+  __syncthreads();
+  constexpr int PT = 32;
+  const uint32_t t0 = threadIdx.x * PT;
+  uint32_t v[PT], sum = 0, tot;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    v[k] = t0 + k < F ? tl[tpad(t0 + k)] : 0u;
+    sum += v[k];
+  }
+  uint32_t acc = block_excl_scan<1024>(sum, lds, &tot);
+#pragma unroll
+  for (int k = 0; k < PT; ++k)
+    if (t0 + k < F) {
+      tl[tpad(t0 + k)] = acc;
+      acc += v[k];
+    }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < F; t += 1024) tile_base[t] = tl[tpad(t)];
+  if (threadIdx.x == 0) tile_base[F] = tot;
+}
+
 __global__ __launch_bounds__(1024) void k_seginfo(const uint32_t* __restrict__ split, const uint32_t* __restrict__ coltot,
                                                   uint32_t F, uint32_t* __restrict__ sinfo) {
   const uint32_t NS = split[0];
@@ -1071,6 +1122,9 @@ hipError_t set_ingest_attributes() {
   const int big = 160 * 1024;
   if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
+  if ((e = hipFuncSetAttribute((const void*)k_tilescan_seg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)((tpad(32768) + 1) * 4))))
+    return e;
   if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)bin1_lds(16384))))
     return e;
@@ -1106,6 +1160,12 @@ hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* coltot, 
 
 hipError_t launch_tilescan(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base, hipStream_t st) {
   hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(1024), 0, st, coltot, F, split, tile_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_tilescan_seg(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base,
+                               uint32_t* sinfo, hipStream_t st) {
+  hipLaunchKernelGGL(k_tilescan_seg, dim3(1), dim3(1024), (tpad(F) + 1) * 4, st, coltot, F, split, tile_base, sinfo);
   return hipGetLastError();
 }
 

@@ -115,6 +115,9 @@ hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uin
 hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* coltot, hipStream_t st);
 // Tile totals (split tiles: sum of their halves, written to coltot[t]) and tile_base[F+1].
 hipError_t launch_tilescan(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base, hipStream_t st);
+// Both of the above and the segment's split info in one workgroup (F <= 32768).
+hipError_t launch_tilescan_seg(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base,
+                               uint32_t* sinfo, hipStream_t st);
 // Segment split info from the batch's split set and half-0 totals.
 hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st);
 // Single-level scatter (batches counted without split tiles).
