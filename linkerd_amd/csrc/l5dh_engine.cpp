@@ -415,9 +415,13 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   }
   State st = state(c);
   Tables tb = tables(c);
+  // a resetting snapshot of every series into dense rows: clean big tiles count
+  // straight into their output rows (no copy of state rows in k_hot_finish)
+  const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S &&
+                         !(c->dbg & 0x8000000);
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_init(pl, hot, st, hc, c->stream));
+    HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, hc, c->stream));
   }
   {
     // cold tiles on the side stream, concurrently with the hot tiles (disjoint
@@ -428,22 +432,22 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
       HIPCHK(c, launch_accum(sv, pl, cold_items, 0, st, tb, out, c->cold_limit, hc, final_mode, reset,
-                             c->side));
+                             direct_out, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, hc, c->stream));
+      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       if (hot_items)
         HIPCHK(c, launch_accum(sv, pl, 0, hot_items, st, tb, out, c->cold_limit, hc, final_mode, reset,
-                               c->stream));
+                               direct_out, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
-      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, hc, c->stream));
+      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, hc, final_mode,
-                             reset, c->stream));
+                             reset, direct_out, c->stream));
     }
   }
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, hc, c->stream));
+    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, direct_out, hc, c->stream));
   }
   c->nseg = 0;
   return 0;

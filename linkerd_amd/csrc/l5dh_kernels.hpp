@@ -167,14 +167,18 @@ hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limi
 // trip for the plan header): the kernels are persistent and read the exact counts
 // from plan.header on the device.  DEV_COUNT as a count: read it on the device.
 constexpr uint32_t DEV_COUNT = 0xFFFFFFFFu;
-hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, uint32_t hot_chunk, hipStream_t st);
+// direct_out (a resetting snapshot of the whole series space into dense device rows):
+// the big tiles that were clean at k_plan count straight into their output rows
+// instead of their state rows, and k_hot_finish summarizes them in place.
+hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, uint32_t hot_chunk,
+                           hipStream_t st);
 hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
-                        hipStream_t st);
+                        int direct_out, hipStream_t st);
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
-                              uint32_t hot_chunk, hipStream_t st);
+                              Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
-                             int reset, uint32_t hot_chunk, hipStream_t st);
+                             int reset, int direct_out, uint32_t hot_chunk, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external
 // dense rows ext[count][1798] + ext_total[count].
 hipError_t launch_rows(State state, const int32_t* ext, const int64_t* ext_total, Tables tb, Outputs out,

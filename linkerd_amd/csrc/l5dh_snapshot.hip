@@ -247,19 +247,40 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   }
 }
 
+// Where a big tile's counts accumulate: its state rows (stride ROW), or -- a clean
+// tile of a resetting full-range snapshot with dense outputs (`direct`) -- its output
+// rows (stride NB), so that k_hot_finish summarizes them in place instead of copying
+// the state rows out (the state rows of a reset clean tile are never read again).
+struct BigRows {
+  uint32_t* base;
+  uint32_t stride;
+};
+__device__ __forceinline__ BigRows big_rows(const State& st, const Outputs& out, const Plan& plan, uint32_t t,
+                                            int direct_out) {
+  if (direct_out && !(plan.tile_flags[t] & TF_DIRTY))
+    return BigRows{reinterpret_cast<uint32_t*>(out.counts + ((size_t)t * TILE - out.first) * NB), (uint32_t)NB};
+  return BigRows{st.counts + (size_t)t * TILE * ROW, (uint32_t)ROW};
+}
+
 // k_hot_init: split tiles accumulate with global atomics into state rows, so
 // clean ones start from zero.
 // Persistent (the number of hot tiles, header[1], is read on the device).
-__global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, uint32_t hot_chunk) {
+__global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, Outputs out, int direct_out, uint32_t hot_chunk) {
   const uint32_t nh = plan.header[1];
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const uint32_t t = plan.hot_list[i];
-    if (st.dirty[t]) continue;
+    if (plan.tile_flags[t] & TF_DIRTY) continue;
     const uint32_t s0 = t * TILE;
     const uint32_t s1 = min(st.S, s0 + TILE);
-    uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
-    const size_t n4 = (size_t)(s1 - s0) * ROW / 4;
-    for (size_t k = threadIdx.x; k < n4; k += 256) p[k] = make_uint4(0, 0, 0, 0);
+    if (direct_out) {  // the output rows: (s1 - s0) x 1798 int32, 8-B aligned
+      uint2* p = reinterpret_cast<uint2*>(out.counts + (size_t)(s0 - out.first) * NB);
+      const size_t n2 = (size_t)(s1 - s0) * NB / 2;
+      for (size_t k = threadIdx.x; k < n2; k += 256) p[k] = make_uint2(0, 0);
+    } else {
+      uint4* p = reinterpret_cast<uint4*>(st.counts + (size_t)s0 * ROW);
+      const size_t n4 = (size_t)(s1 - s0) * ROW / 4;
+      for (size_t k = threadIdx.x; k < n4; k += 256) p[k] = make_uint4(0, 0, 0, 0);
+    }
     if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
   }
 }
@@ -641,7 +662,8 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
 // never reaches 2^16, so it cannot carry into its neighbour); at the end every
 // nonzero bin is flushed with global atomics into the rows k_hot_init cleared, and
 // k_hot_finish summarizes them.  Lane-private u64 value sums.
-__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, uint32_t hot_chunk) {
+__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, Outputs out, int direct_out,
+                                                  uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* hist = smem;                                                                // [32][CROW] u16 pairs
   unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + TILE * CROW);  // [32][64]
@@ -659,7 +681,8 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
     const uint32_t hx = plan.hot_item[item];
     const uint32_t t = hx & 0x7FFFu;
     const uint64_t vlo = (uint64_t)(hx >> 15) * hot_chunk, vhi = vlo + hot_chunk;
-    uint32_t* tile_rows = st.counts + (size_t)t * TILE * ROW;
+    const BigRows br = big_rows(st, out, plan, t, direct_out);
+    uint32_t* tile_rows = br.base;
     auto hist_add = [&](uint32_t loc, uint32_t b) {
       if (g_dbg & 0x2000) return;
       const uint32_t sh = (b & 1u) * 16u;
@@ -667,7 +690,7 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
       const uint32_t old = atomicAdd(wd, 1u << sh);
       if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add made it 2^15: hand 2^15 over
         atomicSub(wd, 0x8000u << sh);
-        atomicAdd(&tile_rows[(size_t)(loc & 31u) * ROW + b], 0x8000u);
+        atomicAdd(&tile_rows[(size_t)(loc & 31u) * br.stride + b], 0x8000u);
       }
     };
     auto sum_add = [&](uint32_t loc, uint32_t v) {
@@ -706,7 +729,7 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
       const uint32_t s = t * TILE + loc;
       if (s >= st.S) continue;
       const uint64_t vsum = wave_sum(vsl[loc * 64 + lane]);
-      uint32_t* grow = tile_rows + (size_t)loc * ROW;
+      uint32_t* grow = tile_rows + (size_t)loc * br.stride;
       const uint32_t* hrow = hist + loc * CROW;
       for (int b0 = 0; b0 < ((g_dbg & 0x1000) ? 0 : NB); b0 += 64) {  // 64 consecutive bins per wave atomic
         const int b = b0 + lane;
@@ -727,7 +750,8 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
 // contiguous range per segment, with no filtering.  u32 LDS bins for the half's
 // 16 series, lane-private value sums, flushed with global atomics (k_hot_init
 // cleared the rows; k_hot_finish summarizes them).
-__global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, uint32_t hot_chunk) {
+__global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                                    int direct_out, uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t nitems = plan.header[3];  // persistent: items blockIdx.x, + gridDim.x, ...
   for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
@@ -784,7 +808,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
   const uint32_t s = t * TILE + 16 * half + w;
   if (s < st.S) {
-    uint32_t* grow = st.counts + (size_t)s * ROW;
+    const BigRows br = big_rows(st, out, plan, t, direct_out);
+    uint32_t* grow = br.base + (size_t)(16 * half + w) * br.stride;
     const uint32_t* hrow = hist + w * HROW;
     for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
       const int b = b0 + lane;
@@ -802,7 +827,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
 // k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
 // write outputs, update state/dirty.
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
-                                                   int reset, uint32_t hot_chunk) {
+                                                   int reset, int direct_out, uint32_t hot_chunk) {
   const uint32_t nv = 2 * plan.header[1];  // persistent: (hot tile, half) pairs
   for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
   const uint32_t t = plan.hot_list[vb >> 1];
@@ -815,10 +840,16 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
     if (final_mode) {
       const uint32_t oi = s - out.first;
       if (s >= out.first && oi < out.count) {
-        const SrcRow32 src{st.counts + (size_t)s * ROW};
         uint32_t g[9];
-        row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
-        wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+        if (direct_out && !(plan.tile_flags[t] & TF_DIRTY)) {  // counted in the output row itself
+          const SrcExt src{out.counts + (size_t)oi * NB};
+          row_pass(src, g, nullptr);
+          wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+        } else {
+          const SrcRow32 src{st.counts + (size_t)s * ROW};
+          row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
+          wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+        }
         if (lane == 0 && out.totals) out.totals[oi] = total;
       }
     }
@@ -930,16 +961,17 @@ static int num_cus() {
   return ncu;
 }
 
-hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, uint32_t hot_chunk, hipStream_t st) {
+hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, uint32_t hot_chunk,
+                           hipStream_t st) {
   if (max_hot == 0) return hipSuccess;
   hipLaunchKernelGGL(k_hot_init, dim3(std::min<uint32_t>(max_hot, 4u * num_cus())), dim3(256), 0, st, plan, state,
-                     hot_chunk);
+                     out, direct_out, hot_chunk);
   return hipGetLastError();
 }
 
 hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_hot_items, State state, Tables tb,
                         Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
-                        hipStream_t st) {
+                        int direct_out, hipStream_t st) {
   const uint32_t ncu = (uint32_t)num_cus();
   if (cold_items) {
     // default: the persistent form, one 1024-thread workgroup per CU walking the cold
@@ -968,25 +1000,25 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_
   }
   if (max_hot_items) {  // persistent: one workgroup per CU walking the chunk items
     hipLaunchKernelGGL(k_accum_hot, dim3(std::min<uint32_t>(max_hot_items, ncu)), dim3(WG), ACC_HOT_LDS, st, segs,
-                       plan, state, tb, hot_chunk);
+                       plan, state, tb, out, direct_out, hot_chunk);
     return hipGetLastError();
   }
   return hipSuccess;
 }
 
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
-                              uint32_t hot_chunk, hipStream_t st) {
+                              Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st) {
   if (max_split_items == 0) return hipSuccess;
   hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, (uint32_t)num_cus())), dim3(WG),
-                     ACC_SPLIT_LDS, st, segs, plan, state, tb, hot_chunk);
+                     ACC_SPLIT_LDS, st, segs, plan, state, tb, out, direct_out, hot_chunk);
   return hipGetLastError();
 }
 
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
-                             int reset, uint32_t hot_chunk, hipStream_t st) {
+                             int reset, int direct_out, uint32_t hot_chunk, hipStream_t st) {
   if (max_hot == 0) return hipSuccess;
   hipLaunchKernelGGL(k_hot_finish, dim3(std::min<uint32_t>(2 * max_hot, 2u * num_cus())), dim3(WG), 0, st, plan, state,
-                     tb, out, final_mode, reset, hot_chunk);
+                     tb, out, final_mode, reset, direct_out, hot_chunk);
   return hipGetLastError();
 }
 
