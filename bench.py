@@ -87,6 +87,7 @@ def parse():
     p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
     p.add_argument("--split-min", type=int, default=None, help="engine param: min records of a split tile")
     p.add_argument("--variant", type=int, default=0, help="engine param L5DH_PARAM_VARIANT (A/B timing; 0: default)")
+    p.add_argument("--hot-chunk", type=int, default=None, help="engine param L5DH_PARAM_HOT_CHUNK (records per big-tile item)")
     p.add_argument("--cpu-sample", type=int, default=None, help="samples in the CPU baseline sample (0: skip)")
     p.add_argument("--cpu-threads", type=int, default=None, help="oracle threads (default: c1 1, else the host's)")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_latest.json"))
@@ -354,7 +355,8 @@ def run(args):
     eng = HistogramEngine(S, device=torch.cuda.current_device())
     eng.set_param(N_.PARAM_BIN_MODE, args.bin_mode)
     for prm, v in ((N_.PARAM_DIRECT_MAX, args.direct_max), (N_.PARAM_DIRECT_DIV, args.direct_div),
-                   (N_.PARAM_SPLIT_MIN, args.split_min), (N_.PARAM_VARIANT, args.variant or None)):
+                   (N_.PARAM_SPLIT_MIN, args.split_min), (N_.PARAM_VARIANT, args.variant or None),
+                   (N_.PARAM_HOT_CHUNK, args.hot_chunk)):
         if v is not None:
             eng.set_param(prm, v)
     if fleet:
