@@ -239,6 +239,56 @@ def test_unsplit_direct_tiles(oracle, mode):
         _assert_summaries_equal(got, o.snapshot(reset=reset), f"unsplit direct {it}")
 
 
+@BIN_MODES
+def test_reset_snapshot_mixed_clean_dirty_big_tiles(oracle, bin_mode):
+    """A resetting full snapshot with dense counts counts the big tiles that were
+    clean at the plan straight into the output rows and copies the dirty ones from
+    state: tile A (series 0-31) split and clean (a range snapshot reset it), tile B
+    (320-351) split and dirty (folded by that range snapshot), tile C (640-671) big,
+    unsplit and clean, several items each, cold tiles everywhere."""
+    rng = np.random.default_rng(41)
+    S = 2000
+    eng = _engine(S, bin_mode)
+    eng.set_param(N.PARAM_COLD_LIMIT, 500)
+    eng.set_param(N.PARAM_HOT_CHUNK, 5000)
+    eng.set_param(N.PARAM_SPLIT_MIN, 1000)
+    o = oracle.OracleHistograms(S)
+
+    def batch(hot, n_hot, n_cold):
+        parts = [rng.integers(lo, lo + 32, n_hot) for lo in hot] + [rng.integers(0, S, n_cold)]
+        series = np.concatenate(parts).astype(np.uint32)
+        rng.shuffle(series)
+        vals = np.exp(3 + 1.2 * rng.standard_normal(series.size)).astype(np.float32)
+        vals[::97] = rng.choice(EDGE_VALUES, size=vals[::97].size)
+        return series, vals
+
+    s0, v0 = batch([0, 320], 30_000, 5_000)  # predicts A and B split for b1
+    eng.ingest(s0, v0)
+    o.ingest(s0, v0)
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts(), err_msg="b0")
+    _assert_summaries_equal(got, o.snapshot(reset=True), "b0")
+    s1, v1 = batch([0, 320], 20_000, 4_000)  # A and B split in b2
+    eng.ingest(s1, v1)
+    a = s1 < 32
+    oa = oracle.OracleHistograms(32)
+    oa.ingest(s1[a], v1[a])
+    o.ingest(s1[~a], v1[~a])
+    _assert_summaries_equal(eng.snapshot(first=0, count=32, reset=True), oa.snapshot(reset=True), "range A")
+    s2, v2 = batch([0, 320, 640], 25_000, 6_000)
+    eng.ingest(s2, v2)
+    o.ingest(s2, v2)
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts(), err_msg="b2")
+    _assert_summaries_equal(got, o.snapshot(reset=True), "b2")
+    s3, v3 = batch([640], 15_000, 3_000)  # after the reset: every tile clean again
+    eng.ingest(s3, v3)
+    o.ingest(s3, v3)
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts(), err_msg="b3")
+    _assert_summaries_equal(got, o.snapshot(reset=True), "b3")
+
+
 @TWO_LEVEL
 def test_big_tile_bins_past_u16(oracle, mode):
     """Big tiles outside the split set (k_accum_hot: whole-tile u16 bins): one bin of
