@@ -502,6 +502,18 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   per = (per + 3) & ~(size_t)3;
   G = (int)((n + per - 1) / per);
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
+  if (c->F == 1 && !(c->variant & 4)) {  // one tile: the samples in input order are its records
+    {
+      KTimer kt(c, L5DH_K_BIN);
+      HIPCHK(c, launch_encode1(ds, dv, n, c->S, tables(c), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, sg.tbase,
+                               c->d_err, vec, c->num_cu, c->stream));
+      HIPCHK(c, launch_seginfo(c->d_nosplit, c->d_tile_tot, c->F, sg.sinfo, c->stream));
+    }
+    sg.n = n;
+    c->nseg++;
+    HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  }
   if (c->bin_mode == 3) {  // paged: no counting pass (l5dh_paged.hip)
     const size_t pp = paged_pool_pages(per);
     if ((double)G * (double)pp * PAGE >= 4294967296.0) return fail(c, -EINVAL, "paged ingest: batch too large");

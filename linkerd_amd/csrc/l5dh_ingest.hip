@@ -333,6 +333,41 @@ __device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int
   return payload1_slow(s, f, tb, sumfix);
 }
 
+// One-tile series spaces (S <= 32: C1, the head shard of a many-way C3): the
+// tile's records are the samples in input order -- no counting pass, no partition.
+// An invalid id becomes 0xFFFFFFFF, which no valid record equals (its bucket field
+// would be 2047) and the accumulate kernels skip; the tile's range is the batch.
+__global__ __launch_bounds__(256) void k_encode1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                                 size_t n, uint32_t S, Tables tb, uint32_t* __restrict__ records,
+                                                 int64_t* __restrict__ sumfix, uint32_t* __restrict__ tile_base,
+                                                 uint32_t* __restrict__ err, int vec) {
+  bool bad = false;
+  auto enc = [&](uint32_t s, float f) -> uint32_t {
+    if (s >= S) {
+      bad = true;
+      return 0xFFFFFFFFu;
+    }
+    return ((s & (TILE - 1)) << 21) | payload1(s, f, tb, sumfix);
+  };
+  const size_t tid = (size_t)blockIdx.x * 256 + threadIdx.x, nth = (size_t)gridDim.x * 256;
+  size_t done = 0;
+  if (vec) {  // 16-B loads and stores
+    const size_t nv = n >> 2;
+    for (size_t i = tid; i < nv; i += nth) {
+      const uint4 a = reinterpret_cast<const uint4*>(series)[i];
+      const float4 v = reinterpret_cast<const float4*>(values)[i];
+      reinterpret_cast<uint4*>(records)[i] = make_uint4(enc(a.x, v.x), enc(a.y, v.y), enc(a.z, v.z), enc(a.w, v.w));
+    }
+    done = nv << 2;
+  }
+  for (size_t i = done + tid; i < n; i += nth) records[i] = enc(series[i], values[i]);
+  if (bad) atomicAdd(err, 1u);  // monotonic, like k_count's
+  if (tid == 0) {
+    tile_base[0] = 0u;
+    tile_base[1] = (uint32_t)n;
+  }
+}
+
 // Single-level: scatter records to the slab's exclusive (slab, tile) segment.
 __global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                             size_t n, size_t per, uint32_t S, uint32_t F,
@@ -1171,6 +1206,16 @@ hipError_t launch_tilescan_seg(uint32_t* coltot, uint32_t F, const uint32_t* spl
 
 hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st) {
   hipLaunchKernelGGL(k_seginfo, dim3(1), dim3(1024), 0, st, split, coltot, F, sinfo);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode1(const uint32_t* series, const float* values, size_t n, uint32_t S, Tables tb,
+                          uint32_t* records, int64_t* sumfix, uint32_t* tile_base, uint32_t* err, bool vec, int num_cu,
+                          hipStream_t st) {
+  const size_t groups = (n + 4 * 256 - 1) / (4 * 256);
+  const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(groups, (size_t)num_cu * 8));
+  hipLaunchKernelGGL(k_encode1, dim3(grid), dim3(256), 0, st, series, values, n, S, tb, records, sumfix, tile_base, err,
+                     vec ? 1 : 0);
   return hipGetLastError();
 }
 

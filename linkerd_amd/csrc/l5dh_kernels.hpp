@@ -120,6 +120,11 @@ hipError_t launch_tilescan_seg(uint32_t* coltot, uint32_t F, const uint32_t* spl
                                uint32_t* sinfo, hipStream_t st);
 // Segment split info from the batch's split set and half-0 totals.
 hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st);
+// One-tile series spaces (F == 1): the records are the samples in input order
+// (invalid ids: 0xFFFFFFFF), tile_base = {0, n}; no counting pass or partition.
+hipError_t launch_encode1(const uint32_t* series, const float* values, size_t n, uint32_t S, Tables tb,
+                          uint32_t* records, int64_t* sumfix, uint32_t* tile_base, uint32_t* err, bool vec, int num_cu,
+                          hipStream_t st);
 // Single-level scatter (batches counted without split tiles).
 hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
                       uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,

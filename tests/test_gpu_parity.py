@@ -365,6 +365,35 @@ def test_invalid_series_reported(oracle, mode):
     _assert_summaries_equal(got, o.snapshot(), "invalid dropped")
 
 
+@pytest.mark.parametrize("variant", [0, 4], ids=["encode1", "partition"])
+@pytest.mark.parametrize("S", [1, 9, 32])
+def test_one_tile_series_space(oracle, S, variant):
+    """S <= 32 (one tile): the samples in input order are the tile's records
+    (k_encode1, no counting pass or partition); variant bit 2 sends the same batches
+    through the partition pipeline.  Invalid ids are dropped and reported, edge
+    values escape, a cold batch and hot multi-item batches, snapshots with and
+    without reset."""
+    rng = np.random.default_rng(60 + S)
+    eng = _engine(S, 2)
+    eng.set_param(N.PARAM_VARIANT, variant)
+    o = oracle.OracleHistograms(S)
+    bad = np.array([S, S + 7, 0xFFFFFFFF], dtype=np.uint32)
+    with pytest.raises(N.L5dhError):
+        eng.ingest(bad, np.ones(3, np.float32))
+        eng.sync()
+    eng.sync()
+    for it, n in enumerate([1, 3_000, 400_001, 1_500_000]):
+        series = rng.integers(0, S, n).astype(np.uint32)
+        vals = np.exp(3 + 1.5 * rng.standard_normal(n)).astype(np.float32)
+        vals[::53] = rng.choice(EDGE_VALUES, size=vals[::53].size)
+        eng.ingest(series, vals)
+        o.ingest(series, vals)
+        reset = it % 2 == 1
+        got, counts = eng.snapshot(reset=reset, with_counts=True)
+        np.testing.assert_array_equal(counts, o.counts(), err_msg=f"batch {it}")
+        _assert_summaries_equal(got, o.snapshot(reset=reset), f"one tile {it}")
+
+
 @BIN_MODES
 def test_c2_slice_bitexact(oracle, bin_mode):
     """C2 recipe at 1/10 of the series: 10k series x 1k samples."""
