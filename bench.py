@@ -65,8 +65,8 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # tiles, split tiles through level 2 and cold tiles cost differently per sample
 COST_PS_PER_SAMPLE = 6.5
 COST_PS_PER_SERIES = 1700.0
-COST_CALIBRATION = ((0, 1.113), (9, 1.0976), (144, 1.2229), (2083, 1.1024), (14736, 1.1316), (72077, 1.1337),
-                    (262409, 1.1106), (585838, 1.1252))  # (first Zipf rank, ms of that r/8 shard)
+COST_CALIBRATION = ((0, 1.0792), (15, 1.0675), (228, 1.0466), (2449, 1.109), (16875, 1.0846), (78438, 1.0927),
+                    (269737, 1.1071), (593489, 1.0959))  # (first Zipf rank, ms of that r/8 shard)
 
 
 def parse():
