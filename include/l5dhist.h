@@ -76,7 +76,8 @@ enum {
   L5DH_PARAM_MERGE_RCCL_1RANK = 11, /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
   L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
                                   every variant computes the same results; bit 1: DMA copies of pinned
-                                  host batches; bit 2: one-tile series spaces through the partition) */
+                                  host batches; bit 2: one-tile series spaces through the partition; bit 3: ... as
+                                  records in input order, instead of folded at ingest) */
 };
 
 /* Fleet-merge modes for l5dh_merge */

@@ -405,6 +405,24 @@ __device__ __forceinline__ uint32_t bucketize(float f, const uint32_t* __restric
   return (key >= 0 && key < INT_MAXV) ? bucket_lut((uint32_t)key, lut, lim) : search_key(key, lim);
 }
 
+// Level-1 payload of a sample outside [0, V_ESC): bucketize, add its exact
+// contribution to sumfix, return V_ESC + bucket (or the truncated value when it
+// lands inside the range after all).  Rare: k_bin1 runs it from a non-unrolled
+// loop so one copy of the full search sits in the hot loop's code.
+__device__ __forceinline__ uint32_t payload1_slow(uint32_t s, float f, Tables tb,
+                                                           int64_t* __restrict__ sumfix) {
+  int64_t c;
+  const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
+  if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
+  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)c);  // whole contribution
+  return V_ESC + b;
+}
+
+__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
+  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
+  return payload1_slow(s, f, tb, sumfix);
+}
+
 // Number of set bits of m below this lane.
 __device__ __forceinline__ uint32_t mask_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

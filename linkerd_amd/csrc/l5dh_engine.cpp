@@ -502,7 +502,16 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   per = (per + 3) & ~(size_t)3;
   G = (int)((n + per - 1) / per);
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
-  if (c->F == 1 && !(c->variant & 4)) {  // one tile: the samples in input order are its records
+  if (c->F == 1 && !(c->variant & 12)) {  // one tile: fold the batch into its state rows now
+    KTimer kt(c, L5DH_K_BIN);
+    const size_t fill = n / (2 * (size_t)std::max(1, c->num_cu));  // >= 2 items per CU when the batch allows
+    const uint32_t chunk =
+        (uint32_t)std::min<size_t>(c->hot_chunk & ~3u, std::max<size_t>(16384, (fill + 1023) & ~(size_t)1023));
+    HIPCHK(c, launch_fold1(ds, dv, n, chunk, state(c), tables(c), c->d_err, vec, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  }
+  if (c->F == 1 && !(c->variant & 4)) {  // (variant bit 3) one tile: the samples in input order are its records
     {
       KTimer kt(c, L5DH_K_BIN);
       HIPCHK(c, launch_encode1(ds, dv, n, c->S, tables(c), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, sg.tbase,

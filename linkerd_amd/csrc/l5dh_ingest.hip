@@ -315,24 +315,6 @@ __global__ __launch_bounds__(1024) void k_seginfo(const uint32_t* __restrict__ s
   }
 }
 
-// Level-1 payload of a sample outside [0, V_ESC): bucketize, add its exact
-// contribution to sumfix, return V_ESC + bucket (or the truncated value when it
-// lands inside the range after all).  Rare: k_bin1 runs it from a non-unrolled
-// loop so one copy of the full search sits in the hot loop's code.
-__device__ __forceinline__ uint32_t payload1_slow(uint32_t s, float f, Tables tb,
-                                                           int64_t* __restrict__ sumfix) {
-  int64_t c;
-  const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
-  if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
-  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)c);  // whole contribution
-  return V_ESC + b;
-}
-
-__device__ __forceinline__ uint32_t payload1(uint32_t s, float f, Tables tb, int64_t* __restrict__ sumfix) {
-  if (f >= 0.0f && f < (float)V_ESC) return (uint32_t)f;
-  return payload1_slow(s, f, tb, sumfix);
-}
-
 // One-tile series spaces (S <= 32: C1, the head shard of a many-way C3): the
 // tile's records are the samples in input order -- no counting pass, no partition.
 // An invalid id becomes 0xFFFFFFFF, which no valid record equals (its bucket field

@@ -744,6 +744,125 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
   }
 }
 
+// One-tile series spaces (S <= 32: C1, the head shard of a many-way C3) fold each
+// batch into the tile's state rows at ingest -- no records, no partition, no
+// segment.  k_fold1_init clears the rows of a clean tile and marks it dirty;
+// k_fold1 items are chunks of the batch, counted like k_accum_hot's (u16-packed
+// LDS bins of the 32 series, a 2^15 hand-off to the state row, nonzero bins flushed
+// with global atomics, lane-private u64 value sums into total; escapes go to sumfix
+// as at ingest).  Invalid ids are dropped and reported like k_count's.
+__global__ __launch_bounds__(256) void k_fold1_init(State st) {
+  const bool clean = st.dirty[0] == 0;
+  if (clean) {
+    uint4* p = reinterpret_cast<uint4*>(st.counts);
+    const size_t n4 = (size_t)st.S * ROW / 4;
+    for (size_t k = threadIdx.x; k < n4; k += 256) p[k] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < st.S) st.total[threadIdx.x] = 0;
+  }
+  __syncthreads();  // every thread has read the flag
+  if (clean && threadIdx.x == 0) st.dirty[0] = 1;
+}
+
+__global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                              size_t n, uint32_t chunk, State st, Tables tb, uint32_t* __restrict__ err,
+                                              int vec) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* hist = smem;                                                                // [32][CROW] u16 pairs
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + TILE * CROW);  // [32][64]
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);                              // [LUT2_N]
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const uint32_t S = st.S;
+  for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
+  bool bad = false;
+  auto enc = [&](uint32_t s, float f) -> uint32_t {
+    if (s >= S) {
+      bad = true;
+      return 0xFFFFFFFFu;
+    }
+    return ((s & (TILE - 1)) << 21) | payload1(s, f, tb, st.sumfix);
+  };
+  auto hist_add = [&](uint32_t loc, uint32_t b) {
+    const uint32_t sh = (b & 1u) * 16u;
+    uint32_t* wd = &hist[(loc & 31u) * CROW + (b >> 1)];
+    const uint32_t old = atomicAdd(wd, 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add made it 2^15: hand 2^15 over
+      atomicSub(wd, 0x8000u << sh);
+      atomicAdd(&st.counts[(size_t)(loc & 31u) * ROW + b], 0x8000u);
+    }
+  };
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 31u) * 64 + lane], (unsigned long long)v); };
+  const size_t nitems = (n + chunk - 1) / chunk;
+  for (size_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    {
+      uint4* q = reinterpret_cast<uint4*>(smem);
+      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const size_t lo = item * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    if (vec) {  // 16-B loads (lo is a multiple of chunk, itself of 4); one group ahead in flight
+      auto ld = [&](size_t g, uint4& sv, uint4& vv) {
+        sv = vv = make_uint4(0u, 0u, 0u, 0u);
+        if (g + 4 <= hi) {
+          sv = *reinterpret_cast<const uint4*>(series + g);
+          vv = *reinterpret_cast<const uint4*>(values + g);
+        } else if (g < hi) {  // the batch's ragged end
+          sv.x = series[g];
+          vv.x = __float_as_uint(values[g]);
+          if (g + 1 < hi) {
+            sv.y = series[g + 1];
+            vv.y = __float_as_uint(values[g + 1]);
+          }
+          if (g + 2 < hi) {
+            sv.z = series[g + 2];
+            vv.z = __float_as_uint(values[g + 2]);
+          }
+        }
+      };
+      size_t g = lo + 4u * threadIdx.x;
+      uint4 s0, v0, s1, v1;
+      ld(g, s0, v0);
+      ld(g + 4u * WG, s1, v1);
+      for (size_t c = lo; c < hi; c += 8u * WG, g += 8u * WG) {
+        const uint4 cs0 = s0, cv0 = v0, cs1 = s1, cv1 = v1;
+        ld(g + 8u * WG, s0, v0);
+        ld(g + 12u * WG, s1, v1);
+        const uint32_t ss[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
+        const uint32_t vv[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const size_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+          x[k] = gk < hi ? enc(ss[k], __uint_as_float(vv[k])) : 0xFFFFFFFFu;
+        }
+        count_batch<8>(x, lut2, hist_add, sum_add);
+      }
+    } else {
+      for (size_t g = lo + threadIdx.x; g < hi; g += WG) {
+        const uint32_t x[1] = {enc(series[g], values[g])};
+        count_batch<1>(x, lut2, hist_add, sum_add);
+      }
+    }
+    __syncthreads();
+    for (int loc = w; loc < TILE; loc += WG / 64) {
+      if ((uint32_t)loc >= S) continue;
+      const uint64_t vsum = wave_sum(vsl[loc * 64 + lane]);
+      uint32_t* grow = st.counts + (size_t)loc * ROW;
+      const uint32_t* hrow = hist + loc * CROW;
+      for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+        const int b = b0 + lane;
+        const uint32_t v = b < NB ? (hrow[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu : 0u;
+        if (__ballot(v != 0u)) {
+          if (v) atomicAdd(&grow[b], v);
+        }
+      }
+      if (lane == 0 && vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[loc]), (unsigned long long)vsum);
+    }
+    __syncthreads();  // the LDS rows are read: the next item may clear them
+  }
+  if (bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
+}
+
 // Split big tiles (split in every pending segment): item = (tile, half, chunk of
 // hot_chunk records of that half).  A segment holds the tile's half-0 records at
 // [tbase, tbase + h0) and its half-1 records after them, so each item reads one
@@ -933,7 +1052,9 @@ hipError_t set_snapshot_attributes() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
+  e = hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_fold1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
@@ -1004,6 +1125,17 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_
     return hipGetLastError();
   }
   return hipSuccess;
+}
+
+hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, uint32_t chunk, State state, Tables tb,
+                       uint32_t* err, bool vec, hipStream_t st) {
+  hipLaunchKernelGGL(k_fold1_init, dim3(1), dim3(256), 0, st, state);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t items = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_fold1, dim3((uint32_t)std::min<size_t>(items, (size_t)num_cus())), dim3(WG), ACC_HOT_LDS, st,
+                     series, values, n, chunk, state, tb, err, vec ? 1 : 0);
+  return hipGetLastError();
 }
 
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,

@@ -365,14 +365,14 @@ def test_invalid_series_reported(oracle, mode):
     _assert_summaries_equal(got, o.snapshot(), "invalid dropped")
 
 
-@pytest.mark.parametrize("variant", [0, 4], ids=["encode1", "partition"])
+@pytest.mark.parametrize("variant", [0, 8, 4], ids=["fold1", "encode1", "partition"])
 @pytest.mark.parametrize("S", [1, 9, 32])
 def test_one_tile_series_space(oracle, S, variant):
-    """S <= 32 (one tile): the samples in input order are the tile's records
-    (k_encode1, no counting pass or partition); variant bit 2 sends the same batches
-    through the partition pipeline.  Invalid ids are dropped and reported, edge
-    values escape, a cold batch and hot multi-item batches, snapshots with and
-    without reset."""
+    """S <= 32 (one tile): each batch is folded into the tile's state rows at ingest
+    (k_fold1); variant bit 3 makes the samples in input order the tile's records
+    instead (k_encode1), bit 2 sends the batches through the partition pipeline.
+    Invalid ids are dropped and reported, edge values escape, a cold batch and hot
+    multi-item batches, snapshots with and without reset."""
     rng = np.random.default_rng(60 + S)
     eng = _engine(S, 2)
     eng.set_param(N.PARAM_VARIANT, variant)
@@ -382,7 +382,8 @@ def test_one_tile_series_space(oracle, S, variant):
         eng.ingest(bad, np.ones(3, np.float32))
         eng.sync()
     eng.sync()
-    for it, n in enumerate([1, 3_000, 400_001, 1_500_000]):
+    eng.set_param(N.PARAM_HOT_CHUNK, 100_000)  # several items per batch, a ragged last one
+    for it, n in enumerate([1, 3_000, 400_001, 1_500_000, 262_147]):
         series = rng.integers(0, S, n).astype(np.uint32)
         vals = np.exp(3 + 1.5 * rng.standard_normal(n)).astype(np.float32)
         vals[::53] = rng.choice(EDGE_VALUES, size=vals[::53].size)
