@@ -64,9 +64,16 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # (the sweep profiles/r02q_shards_before.jsonl, after the stream-ordered snapshot): direct
 # tiles, split tiles through level 2 and cold tiles cost differently per sample
 COST_PS_PER_SAMPLE = 6.5
+ONE_TILE = 32  # series of one tile: such a series space is folded at ingest (k_fold1)
+# the first tile as one shard, folded at ingest (ms, `--shard 0/8` of the pinned plan); the
+# calibration's first entry prices it partitioned (1.28 ms measured for its first 15 series)
+COST_FIRST_TILE_FOLDED = 0.8274
 COST_PS_PER_SERIES = 1700.0
-COST_CALIBRATION = ((0, 1.0792), (15, 1.0675), (228, 1.0466), (2449, 1.109), (16875, 1.0846), (78438, 1.0927),
-                    (269737, 1.1071), (593489, 1.0959))  # (first Zipf rank, ms of that r/8 shard)
+COST_CALIBRATION = ((0, 1.5), (32, 1.0543), (438, 1.0466), (4084, 1.0721), (22645, 1.0502), (99791, 1.034),
+                    (300417, 1.0519), (615688, 1.0599))  # (first Zipf rank, ms of that r/8 shard)
+# the same from the 4- and 2-way sweeps (a plan of W ranks uses the sweep of W, else the 8-way one)
+COST_CALIBRATION_W = {4: ((0, 2.2185), (190, 2.1285), (15832, 2.0186), (272830, 2.0488)),
+                      2: ((0, 4.1812), (15832, 3.8621))}
 
 
 def parse():
@@ -130,7 +137,7 @@ def plan(args, world: int, rank: int) -> dict:
         # balanced by expected device time: COST_PS_PER_SAMPLE per Zipf-expected
         # sample + COST_PS_PER_SERIES per series row (balancing by samples alone
         # would leave the last rank most of the dense series rows)
-        shards = fleet.shard_ranges(S, world, weights=shard_cost(cdf, N))
+        shards = shard_plan(S, N, world, cdf)
         sh = shards[rank]
         mass = [float(cdf[x.first + x.count - 1] - (cdf[x.first - 1] if x.first else 0.0)) if x.count else 0.0
                 for x in shards]
@@ -148,15 +155,37 @@ def plan(args, world: int, rank: int) -> dict:
                 base_index=0, world=world, rank=rank, scaling="weak")
 
 
-def shard_cost(cdf, N):
+def shard_plan(S, N, world, cdf):
+    """C3 series ranges of equal expected device time.  A one-tile head shard is
+    folded at ingest (k_fold1, about half the device time per sample of a
+    partitioned shard, but only while it holds <= ONE_TILE series): the plan pins
+    rank 0 to the first tile when that lowers the expected slowest rank, else it
+    balances every rank over the partitioned costs."""
+    from linkerd_amd import fleet
+    w = shard_cost(cdf, N, world)  # partitioned costs, the first tile included
+    plain = fleet.shard_ranges(S, world, weights=w)
+    if world == 1 or S <= ONE_TILE:
+        return plain
+    cost = lambda x: float(w[x.first:x.first + x.count].sum())
+    calibrated = S == S_C3 and N == N_C3
+    folded = COST_FIRST_TILE_FOLDED if calibrated else 0.5 * float(w[:ONE_TILE].sum())
+    rest = fleet.shard_ranges(S - ONE_TILE, world - 1, weights=w[ONE_TILE:])
+    pinned = [fleet.Shard(0, 0, ONE_TILE)] + [fleet.Shard(x.rank + 1, x.first + ONE_TILE, x.count) for x in rest]
+    if max([folded] + [cost(x) for x in pinned[1:]]) < max(cost(x) for x in plain):
+        return pinned
+    return plain
+
+
+def shard_cost(cdf, N, world=8):
     """Expected device time per series of the C3 workload (COST_* above)."""
     import numpy as np
     S = cdf.size
     pmf = np.diff(np.concatenate([[0.0], cdf]))
     w = COST_PS_PER_SAMPLE * N * pmf + COST_PS_PER_SERIES
     if S == S_C3 and N == N_C3:  # the calibration is of this workload
-        edges = [a for a, _ in COST_CALIBRATION] + [S]
-        for (a, ms), b in zip(COST_CALIBRATION, edges[1:]):
+        cal = COST_CALIBRATION_W.get(world, COST_CALIBRATION)
+        edges = [a for a, _ in cal] + [S]
+        for (a, ms), b in zip(cal, edges[1:]):
             w[a:b] *= ms / w[a:b].sum()
     return w
 

@@ -34,9 +34,28 @@ def test_c3_ranks_cover_the_series_space(gpus):
     sys.path.insert(0, REPO)
     import bench
     from linkerd_amd import synth
-    w = bench.shard_cost(synth.zipf_cdf(1_000_000), 1_000_000_000)
+    w = bench.shard_cost(synth.zipf_cdf(1_000_000), 1_000_000_000, gpus)
     cost = [w[p["first"]:p["first"] + p["count"]].sum() for p in plans]
     assert max(cost) / min(cost) < 1.02
+
+
+def test_c3_eight_way_plan_pins_the_folded_first_tile():
+    """8 ranks: rank 0 holds exactly the first tile (one tile is folded at ingest,
+    k_fold1), the other 7 split the rest with equal modelled device time; 2 and 4
+    ranks keep a partitioned head shard."""
+    sys.path.insert(0, REPO)
+    import bench
+    from linkerd_amd import synth
+    cdf = synth.zipf_cdf(1_000_000)
+    sh = bench.shard_plan(1_000_000, 1_000_000_000, 8, cdf)
+    assert (sh[0].first, sh[0].count) == (0, bench.ONE_TILE)
+    assert sum(x.count for x in sh) == 1_000_000 and all(b.first == a.first + a.count for a, b in zip(sh, sh[1:]))
+    w = bench.shard_cost(cdf, 1_000_000_000, 8)
+    cost = [w[x.first:x.first + x.count].sum() for x in sh[1:]]
+    assert max(cost) / min(cost) < 1.02
+    assert bench.COST_FIRST_TILE_FOLDED < min(cost)
+    for world in (2, 4):
+        assert bench.shard_plan(1_000_000, 1_000_000_000, world, cdf)[0].count > bench.ONE_TILE
 
 
 def test_c4_ranks_split_the_samples():
