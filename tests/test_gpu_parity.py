@@ -365,16 +365,17 @@ def test_invalid_series_reported(oracle, mode):
     _assert_summaries_equal(got, o.snapshot(), "invalid dropped")
 
 
+@pytest.mark.parametrize("stage", [0, None], ids=["unstaged", "ring"])
 @pytest.mark.parametrize("variant", [0, 8, 4], ids=["fold1", "encode1", "partition"])
 @pytest.mark.parametrize("S", [1, 9, 32])
-def test_one_tile_series_space(oracle, S, variant):
+def test_one_tile_series_space(oracle, S, variant, stage):
     """S <= 32 (one tile): each batch is folded into the tile's state rows at ingest
     (k_fold1); variant bit 3 makes the samples in input order the tile's records
     instead (k_encode1), bit 2 sends the batches through the partition pipeline.
     Invalid ids are dropped and reported, edge values escape, a cold batch and hot
     multi-item batches, snapshots with and without reset."""
     rng = np.random.default_rng(60 + S)
-    eng = _engine(S, 2)
+    eng = _engine(S, 2, stage=stage)
     eng.set_param(N.PARAM_VARIANT, variant)
     o = oracle.OracleHistograms(S)
     bad = np.array([S, S + 7, 0xFFFFFFFF], dtype=np.uint32)
