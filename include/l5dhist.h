@@ -75,7 +75,8 @@ enum {
   L5DH_PARAM_MAX_SLABS = 10,   /* ingest slabs (workgroups of the partition kernels), 1..512 */
   L5DH_PARAM_MERGE_RCCL_1RANK = 11, /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
   L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
-                                  every variant computes the same results; bit 1: DMA copies of pinned
+                                  every variant computes the same results; bit 0: k_bin1 without the ballot
+                                  ranking of hot bins, and one-tile folds in u16 bins; bit 1: DMA copies of pinned
                                   host batches; bit 2: one-tile series spaces through the partition; bit 3: ... as
                                   records in input order, instead of folded at ingest) */
 };

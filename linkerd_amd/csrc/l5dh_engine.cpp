@@ -507,7 +507,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     const size_t fill = n / (2 * (size_t)std::max(1, c->num_cu));  // >= 2 items per CU when the batch allows
     const uint32_t chunk =
         (uint32_t)std::min<size_t>(c->hot_chunk & ~3u, std::max<size_t>(16384, (fill + 1023) & ~(size_t)1023));
-    HIPCHK(c, launch_fold1(ds, dv, n, chunk, state(c), tables(c), c->d_err, vec, c->stream));
+    HIPCHK(c, launch_fold1(ds, dv, n, chunk, state(c), tables(c), c->d_err, vec, (c->variant & 1) != 0, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     return 0;
   }

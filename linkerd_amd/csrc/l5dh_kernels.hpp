@@ -123,9 +123,10 @@ hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_
 // One-tile series spaces (F == 1): the records are the samples in input order
 // (invalid ids: 0xFFFFFFFF), tile_base = {0, n}; no counting pass or partition.
 // ... or folded into the tile's state rows at ingest (k_fold1_init + k_fold1, chunks of
-// `chunk` samples, a multiple of 4), with no records or segment.
+// `chunk` samples, a multiple of 4), with no records or segment.  S <= 16: u32 LDS
+// bins (wide: the 32-series u16 kernel anyway, A/B).
 hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, uint32_t chunk, State state, Tables tb,
-                       uint32_t* err, bool vec, hipStream_t st);
+                       uint32_t* err, bool vec, bool wide, hipStream_t st);
 hipError_t launch_encode1(const uint32_t* series, const float* values, size_t n, uint32_t S, Tables tb,
                           uint32_t* records, int64_t* sumfix, uint32_t* tile_base, uint32_t* err, bool vec, int num_cu,
                           hipStream_t st);

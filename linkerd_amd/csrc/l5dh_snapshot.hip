@@ -750,7 +750,8 @@ __global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st
 // k_fold1 items are chunks of the batch, counted like k_accum_hot's (u16-packed
 // LDS bins of the 32 series, a 2^15 hand-off to the state row, nonzero bins flushed
 // with global atomics, lane-private u64 value sums into total; escapes go to sumfix
-// as at ingest).  Invalid ids are dropped and reported like k_count's.
+// as at ingest).  Invalid ids are dropped and reported like k_count's.  W32: at most
+// 16 series (C1), u32 LDS bins (non-returning atomics, no hand-off).
 __global__ __launch_bounds__(256) void k_fold1_init(State st) {
   const bool clean = st.dirty[0] == 0;
   if (clean) {
@@ -763,13 +764,16 @@ __global__ __launch_bounds__(256) void k_fold1_init(State st) {
   if (clean && threadIdx.x == 0) st.dirty[0] = 1;
 }
 
+template <bool W32>
 __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                               size_t n, uint32_t chunk, State st, Tables tb, uint32_t* __restrict__ err,
                                               int vec) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* hist = smem;                                                                // [32][CROW] u16 pairs
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + TILE * CROW);  // [32][64]
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);                              // [LUT2_N]
+  constexpr int NSER = W32 ? 16 : TILE;
+  constexpr int RW = W32 ? HROW : CROW;                                                 // LDS words per series row
+  uint32_t* hist = smem;                                                                // [NSER][RW] u32 / u16 pairs
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + NSER * RW);    // [NSER][64]
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);                              // [LUT2_N]
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const uint32_t S = st.S;
@@ -783,6 +787,10 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
     return ((s & (TILE - 1)) << 21) | payload1(s, f, tb, st.sumfix);
   };
   auto hist_add = [&](uint32_t loc, uint32_t b) {
+    if (W32) {
+      atomicAdd(&hist[(loc & (NSER - 1)) * RW + b], 1u);
+      return;
+    }
     const uint32_t sh = (b & 1u) * 16u;
     uint32_t* wd = &hist[(loc & 31u) * CROW + (b >> 1)];
     const uint32_t old = atomicAdd(wd, 1u << sh);
@@ -791,12 +799,14 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
       atomicAdd(&st.counts[(size_t)(loc & 31u) * ROW + b], 0x8000u);
     }
   };
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 31u) * 64 + lane], (unsigned long long)v); };
+  auto sum_add = [&](uint32_t loc, uint32_t v) {
+    atomicAdd(&vsl[(loc & (NSER - 1)) * 64 + lane], (unsigned long long)v);
+  };
   const size_t nitems = (n + chunk - 1) / chunk;
   for (size_t item = blockIdx.x; item < nitems; item += gridDim.x) {
     {
       uint4* q = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < (NSER * RW + NSER * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const size_t lo = item * chunk, hi = lo + chunk < n ? lo + chunk : n;
@@ -844,14 +854,14 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
       }
     }
     __syncthreads();
-    for (int loc = w; loc < TILE; loc += WG / 64) {
+    for (int loc = w; loc < NSER; loc += WG / 64) {
       if ((uint32_t)loc >= S) continue;
       const uint64_t vsum = wave_sum(vsl[loc * 64 + lane]);
       uint32_t* grow = st.counts + (size_t)loc * ROW;
-      const uint32_t* hrow = hist + loc * CROW;
+      const uint32_t* hrow = hist + loc * RW;
       for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
         const int b = b0 + lane;
-        const uint32_t v = b < NB ? (hrow[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu : 0u;
+        const uint32_t v = b >= NB ? 0u : W32 ? hrow[b] : (hrow[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu;
         if (__ballot(v != 0u)) {
           if (v) atomicAdd(&grow[b], v);
         }
@@ -1054,7 +1064,9 @@ hipError_t set_snapshot_attributes() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_fold1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
+  e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
@@ -1128,13 +1140,18 @@ hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_
 }
 
 hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, uint32_t chunk, State state, Tables tb,
-                       uint32_t* err, bool vec, hipStream_t st) {
+                       uint32_t* err, bool vec, bool wide, hipStream_t st) {
   hipLaunchKernelGGL(k_fold1_init, dim3(1), dim3(256), 0, st, state);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t items = (n + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_fold1, dim3((uint32_t)std::min<size_t>(items, (size_t)num_cus())), dim3(WG), ACC_HOT_LDS, st,
-                     series, values, n, chunk, state, tb, err, vec ? 1 : 0);
+  const dim3 grid((uint32_t)std::min<size_t>(items, (size_t)num_cus()));
+  if (state.S <= 16 && !wide)
+    hipLaunchKernelGGL(k_fold1<true>, grid, dim3(WG), ACC_SPLIT_LDS, st, series, values, n, chunk, state, tb, err,
+                       vec ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_fold1<false>, grid, dim3(WG), ACC_HOT_LDS, st, series, values, n, chunk, state, tb, err,
+                       vec ? 1 : 0);
   return hipGetLastError();
 }
 

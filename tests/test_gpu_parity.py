@@ -366,11 +366,12 @@ def test_invalid_series_reported(oracle, mode):
 
 
 @pytest.mark.parametrize("stage", [0, None], ids=["unstaged", "ring"])
-@pytest.mark.parametrize("variant", [0, 8, 4], ids=["fold1", "encode1", "partition"])
+@pytest.mark.parametrize("variant", [0, 1, 8, 4], ids=["fold1", "fold1_u16", "encode1", "partition"])
 @pytest.mark.parametrize("S", [1, 9, 32])
 def test_one_tile_series_space(oracle, S, variant, stage):
     """S <= 32 (one tile): each batch is folded into the tile's state rows at ingest
-    (k_fold1); variant bit 3 makes the samples in input order the tile's records
+    (k_fold1: u32 bins up to 16 series, else -- and with variant bit 0 -- the u16 bins
+    with the 2^15 hand-off); variant bit 3 makes the samples in input order the tile's records
     instead (k_encode1), bit 2 sends the batches through the partition pipeline.
     Invalid ids are dropped and reported, edge values escape, a cold batch and hot
     multi-item batches, snapshots with and without reset."""
