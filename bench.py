@@ -89,10 +89,9 @@ def parse():
     p.add_argument("--shard", default=None, help="r/W: run rank r's C3 shard of a W-way split on this one GPU")
     p.add_argument("--series", type=int, default=None, help="series (default: workload's)")
     p.add_argument("--samples", type=int, default=None, help="samples per step in total (default: workload's)")
-    p.add_argument("--bin-mode", type=int, default=0)
+    p.add_argument("--region-pct", type=int, default=None, help="engine param: region capacity percent (redo path below 100)")
     p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..255)")
     p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
-    p.add_argument("--split-min", type=int, default=None, help="engine param: min records of a split tile")
     p.add_argument("--variant", type=int, default=0, help="engine param L5DH_PARAM_VARIANT (A/B timing; 0: default)")
     p.add_argument("--hot-chunk", type=int, default=None, help="engine param L5DH_PARAM_HOT_CHUNK (records per big-tile item)")
     p.add_argument("--cpu-sample", type=int, default=None, help="samples in the CPU baseline sample (0: skip)")
@@ -252,12 +251,16 @@ def java_probe() -> str:
         return f"java present but -version failed: {e}"
 
 
-def cpu_baseline(pl, sample, threads):
+def cpu_baseline(pl, sample, thread_counts):
     """C oracle (restatement of the JVM Metric.Stat path: per-series mutex, binary
-    search, int32[1798] per series, 8-scan summary) on a bounded sample of the same
-    recipe: `sample` samples ingested with `threads` workers, then all series
-    snapshot on ONE thread (the timer thread, AdminMetricsExportTelemeter.scala:154-162),
-    extrapolated to one full step."""
+    search, int32[1798] per series, 8-scan summary) on the same recipe: `sample`
+    samples ingested with each thread count of `thread_counts` (a thread takes a
+    contiguous slice of the COO stream and locks the series of each sample, as the
+    Finagle worker threads lock each Stat, Metric.scala:30-33), then all series
+    snapshot on ONE thread (the timer thread, AdminMetricsExportTelemeter.scala:154-162).
+    A sample smaller than the step is extrapolated to one full step (said so in
+    `sample`).  The entry with the most threads is the headline `value`; every count
+    is listed in `by_threads`."""
     from linkerd_amd import synth
     from oracle import oracle as O
     wl, S, N = pl["workload"], pl["count"], pl["samples"]
@@ -269,21 +272,28 @@ def cpu_baseline(pl, sample, threads):
         n = s.size
     else:
         s, v = synth.c1(n=n)
-    h = O.OracleHistograms(S)
-    h.ingest(s[: min(n, 100_000)], v[: min(n, 100_000)], threads=threads)  # first-touch warmup
-    h = O.OracleHistograms(S)
-    t0 = time.perf_counter()
-    assert h.ingest(s, v, threads=threads) == 0
-    t_ing = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    h.snapshot(reset=True)
-    t_snap = time.perf_counter() - t0
-    full = t_ing * (N / n) + t_snap
-    model, nproc, avail, _ = host_cpu()
-    return {"value": N / full, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{wl} recipe, {n} samples ingested with {threads} thread(s) ({t_ing:.2f} s) + snapshot of all "
-                      f"{S} series on 1 thread ({t_snap:.2f} s), extrapolated to {N} samples/step",
-            "cpu_model": model, "nproc": nproc, "cpus_available": avail, "java": java_probe(),
+    runs = []
+    for threads in thread_counts:
+        h = O.OracleHistograms(S)
+        h.ingest(s[: min(n, 100_000)], v[: min(n, 100_000)], threads=threads)  # first-touch warmup
+        h = O.OracleHistograms(S)
+        t0 = time.perf_counter()
+        assert h.ingest(s, v, threads=threads) == 0
+        t_ing = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        h.snapshot(reset=True)
+        t_snap = time.perf_counter() - t0
+        full = t_ing * (N / n) + t_snap
+        del h
+        runs.append({"threads": threads, "value": N / full, "ingest_s": round(t_ing, 3), "snapshot_s": round(t_snap, 3)})
+    best = max(runs, key=lambda r: r["threads"])
+    model, nproc, avail, share = host_cpu()
+    extra = "" if n == N else f", extrapolated to {N} samples/step"
+    return {"value": best["value"], "unit": "samples/s", "cores": best["threads"], "kind": "port",
+            "sample": (f"{wl} recipe, {n} samples ingested with " + " / ".join(f"{r['threads']}" for r in runs) +
+                       f" thread(s) + snapshot of all {S} series on 1 thread{extra}"),
+            "by_threads": runs, "cpu_model": model, "nproc": nproc, "cpus_available": avail, "cpu_share": share,
+            "java": java_probe(),
             "note": "C restatement of the JVM path (oracle/hist_oracle.c); no JDK/finagle-stats jar on the box"}
 
 
@@ -382,9 +392,8 @@ def run(args):
     n = pl["samples"]
 
     eng = HistogramEngine(S, device=torch.cuda.current_device())
-    eng.set_param(N_.PARAM_BIN_MODE, args.bin_mode)
     for prm, v in ((N_.PARAM_DIRECT_MAX, args.direct_max), (N_.PARAM_DIRECT_DIV, args.direct_div),
-                   (N_.PARAM_SPLIT_MIN, args.split_min), (N_.PARAM_VARIANT, args.variant or None),
+                   (N_.PARAM_REGION_PCT, args.region_pct), (N_.PARAM_VARIANT, args.variant or None),
                    (N_.PARAM_HOT_CHUNK, args.hot_chunk)):
         if v is not None:
             eng.set_param(prm, v)
@@ -395,6 +404,9 @@ def run(args):
             eng.comm_init_rank(obj[0], world, rank)
         else:
             eng.comm_init_rank(HistogramEngine.comm_unique_id(), 1, 0)
+            # one rank: run the sparse exchange (encode, RCCL send/recv to itself, decode)
+            # instead of skipping it, so its bytes and time are measured
+            eng.set_param(N_.PARAM_MERGE_RCCL_1RANK, 1)
     rows = eng.merge_rows() if fleet else S
     summ = torch.empty((max(rows, 1), 11), dtype=torch.int64, device=dev)
     counts = None if fleet else torch.empty((max(S, 1), N_.NBUCKETS), dtype=torch.int32, device=dev)
@@ -514,21 +526,36 @@ def run(args):
                     "pricing": "SURVEY.md §8d: bin1 8 B/sample, accum 7280 B/series (7192 for the c4 export)"}
     # path: B_alg of everything this step processed, over the step time and all GPUs' peak
     rows_summarized = pl["S_total"] if not args.shard else S
+    world_c4 = pl["world"] if fleet else 1  # (--shard r/W: the W-rank merge this rank's share belongs to)
     balg = 8 * (total_samples if not args.shard else n) + 7280 * rows_summarized
     gpus = 1 if args.shard else world
     path_gbs = balg / (ms_per_step * 1e-3) / 1e9
     merge = None
-    if fleet and "merge" in kt and kt["merge"][1]:
-        cms = kt["merge"][0] / kt["merge"][1]
-        nbytes = eng.merge_rows() * world * (N_.NBUCKETS * 4 + 8)
-        merge = {"collective": "RCCL reduce-scatter (l5dh_merge)" if world > 1 else "RCCL reduce-scatter, 1 rank",
-                 "collective_ms": round(cms, 4), "bytes_per_rank": nbytes,
-                 "bus_GBs": round(nbytes * (world - 1) / world / (cms * 1e-3) / 1e9, 1) if world > 1 else None}
+    if fleet:
+        mb = eng.merge_bytes()
+        cms = kt["merge"][0] / kt["merge"][1] if "merge" in kt and kt["merge"][1] else None
+        merge = {"collective": "sparse reduce-scatter over RCCL send/recv + int64 reduce-scatter of the totals (l5dh_merge)",
+                 "collective_ms": round(cms, 4) if cms else None,
+                 "bytes_per_rank": mb["sent"] if world > 1 else mb["encoded"] * (world_c4 - 1) // world_c4,
+                 "dense_bytes_per_rank": mb["dense"] * (world_c4 - 1) // world_c4,
+                 "encoded_bytes": mb["encoded"], "dense_bytes": mb["dense"],
+                 "encoded_over_dense": round(mb["encoded"] / mb["dense"], 4) if mb["dense"] else None,
+                 "note": (f"bytes per rank of a {world_c4}-rank merge: (W-1)/W of this rank's sparse encoding "
+                          "(entries + words per row + totals) against (W-1)/W of the dense rows + totals; at one "
+                          "rank the exchange runs through RCCL to itself (L5DH_PARAM_MERGE_RCCL_1RANK)")}
     cpu = None
-    sample = args.cpu_sample if args.cpu_sample is not None else (10_000_000 if pl["workload"] == "c1" else 20_000_000)
+    # C1 and C2: the whole step (no extrapolation); C3: a bounded sample of the step
+    default_sample = {"c1": n, "c2": n}.get(pl["workload"], 50_000_000)
+    sample = args.cpu_sample if args.cpu_sample is not None else default_sample
     if rank == 0 and world == 1 and sample > 0 and not streaming:
-        threads = args.cpu_threads or (1 if pl["workload"] == "c1" else host_cpu()[3])
-        cpu = cpu_baseline(pl, sample, threads)
+        _, nproc, avail, share = host_cpu()
+        if args.cpu_threads:
+            tcounts = [args.cpu_threads]
+        elif pl["workload"] == "c1":
+            tcounts = [1]  # one Stat: every add serializes on its monitor (Metric.scala:30-33)
+        else:
+            tcounts = sorted({share, avail})  # the GPU's CPU share and every core of the box
+        cpu = cpu_baseline(pl, sample, tcounts)
     if rank == 0:
         wl_names = {"c3": "C3: 1M series, 1e9 Zipf(s=1) samples per step, log-normal values",
                     "c2": "C2: 100k series x 1k samples, permuted COO",
@@ -542,7 +569,7 @@ def run(args):
                                f"series-sharded x{world} (weighted ranges)" if pl["workload"] == "c3" else
                                f"replicas x{world}"),
                "step": ("ingest + l5dh_merge (export, reduce-scatter, slice summaries)" if fleet else
-                        "ingest (count+scan+bin1+bin2) + snapshot(reset, dense counts + summaries)")}
+                        "ingest (sample+plan+bin1+bin2) + snapshot(reset, dense counts + summaries)")}
         if distributed and backend != "nccl":
             cfg["rehearsal"] = (f"{backend} rank harness, {world} ranks on {torch.cuda.device_count()} GPU(s): "
                                 "not a scaling number")

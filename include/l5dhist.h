@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define L5DH_ABI_VERSION 2 /* 2: staging ring, deferred id errors, RCCL merge, NULL = null stream */
+#define L5DH_ABI_VERSION 3 /* 3: count-free partition (no bin-mode / split-min tunables); id errors from l5dh_sync only */
 #define L5DH_NLIMITS 1797  /* BucketedHistogram.scala:42 (0.5% error => 1797 limits) */
 #define L5DH_NBUCKETS 1798 /* counts = limits.length + 1 (upstream finagle-stats) */
 #define L5DH_MAX_SERIES (1u << 20) /* per context (= per GPU); shard wider fleets */
@@ -65,20 +65,19 @@ typedef struct {
 enum {
   L5DH_PARAM_TIMING = 1,      /* 1: record HIP events around every kernel launch */
   L5DH_PARAM_COLD_LIMIT = 2,  /* max records for the single-pass tile path (<= 65535) */
-  L5DH_PARAM_HOT_CHUNK = 3,   /* max records per work item on the big-tile paths, 1024..2^20 (fewer when CUs would idle) */
+  L5DH_PARAM_HOT_CHUNK = 3,   /* max records per work item on the big-tile path, 1024..2^20 (fewer when CUs would idle) */
   L5DH_PARAM_MAX_SEGMENTS = 4, /* binned ingest batches kept before folding (1..8) */
-  L5DH_PARAM_BIN_MODE = 5,     /* 0 auto (= 2), 1 single-level scatter, 2 two-level partition, 3 paged two-level (no counting pass) */
-  L5DH_PARAM_DIRECT_MAX = 6,   /* tiles whose final records k_bin1 writes directly (0..255) */
-  L5DH_PARAM_DIRECT_DIV = 7,   /* direct tiles average >= 1/div records per 8K-sample sub-chunk */
-  L5DH_PARAM_SPLIT_MIN = 8,    /* tiles laid out per half-tile have >= this many records per batch */
+  L5DH_PARAM_DIRECT_MAX = 6,   /* tiles whose final records level 1 writes directly (0..255) */
+  L5DH_PARAM_DIRECT_DIV = 7,   /* direct tiles hold >= 1/div records per 8K samples of the batch */
   L5DH_PARAM_STAGE_SAMPLES = 9, /* device staging ring for small batches, in samples (0: off) */
-  L5DH_PARAM_MAX_SLABS = 10,   /* ingest slabs (workgroups of the partition kernels), 1..512 */
+  L5DH_PARAM_MAX_SLABS = 10,   /* ingest slabs (workgroups of the level-1 kernel), 1..512 */
   L5DH_PARAM_MERGE_RCCL_1RANK = 11, /* 1: run the RCCL collective even in a 1-rank communicator (tests) */
+  L5DH_PARAM_REGION_PCT = 13,  /* capacity of the partition's regions in percent of the prediction (1..1000,
+                                  default 100); a region that overflows is redone with exact sizes, so values
+                                  below 100 exercise that path (tests) and cost time, never results */
   L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
-                                  every variant computes the same results; bit 0: k_bin1 without the ballot
-                                  ranking of hot bins, and one-tile folds in u16 bins; bit 1: DMA copies of pinned
-                                  host batches; bit 2: one-tile series spaces through the partition; bit 3: ... as
-                                  records in input order, instead of folded at ingest) */
+                                  every variant computes the same results; bit 0: one-tile folds in u16 bins;
+                                  bit 1: DMA copies of pinned host batches) */
 };
 
 /* Fleet-merge modes for l5dh_merge */
@@ -90,13 +89,13 @@ enum {
 
 /* Kernel ids for l5dh_kernel_time */
 enum {
-  L5DH_K_COUNT = 0,  /* per-slab tile histogram of the batch */
-  L5DH_K_SCAN = 1,   /* slab/tile offset scans and the snapshot plan */
-  L5DH_K_BIN = 2,    /* level-1 partition by super-tile (or the single-level bin) */
+  L5DH_K_COUNT = 0,  /* (unused: the partition has no counting pass) */
+  L5DH_K_SCAN = 1,   /* the batch sample, the partition plans and the snapshot plan */
+  L5DH_K_BIN = 2,    /* level-1 partition by super-tile and direct half-tile (+ its redo) */
   L5DH_K_ACCUM = 3,  /* LDS-private tile histograms + fused summary / dense flush */
-  L5DH_K_HOT = 4,    /* split-tile init/finish and row summaries */
+  L5DH_K_HOT = 4,    /* big-tile init/finish and row summaries */
   L5DH_K_COPY = 5,   /* H2D/D2H staging copies */
-  L5DH_K_BIN2 = 6,   /* level-2 partition (super-tile runs -> per-tile segments) */
+  L5DH_K_BIN2 = 6,   /* level-2 partition (super-tile regions -> 16-bit per-key records, + its redo) */
   L5DH_K_MERGE = 7,  /* the RCCL collective of l5dh_merge */
   L5DH_K_NKERNELS = 8
 };
@@ -123,10 +122,12 @@ const int32_t* l5dh_limits(size_t* n);
  * may be reused once it returns when the context runs on its own stream, and
  * in stream order when it runs on a caller stream (l5dh_set_stream).
  *
- * Samples with out-of-range ids are dropped.  The kernels detect them
- * asynchronously: the error is reported as -EINVAL by a later l5dh_ingest
- * (once the device has flagged it) or at the latest by l5dh_sync, once per
- * occurrence; all valid samples are ingested. */
+ * Returns 0 once the batch is accepted (queued), otherwise an error and nothing
+ * of the batch was queued.  Samples with out-of-range ids are dropped; the kernels
+ * detect them asynchronously and l5dh_sync reports -EINVAL for them (a
+ * later ingest never carries an earlier batch's error: an error from l5dh_ingest
+ * means this batch was not queued -- or, for a batch above 2^30 samples, only its
+ * leading 2^30-sample pieces were); all valid samples are ingested. */
 int l5dh_ingest(l5dh_ctx* ctx, const uint32_t* series, const float* values, size_t n);
 
 /* The same without waiting for the copy of host buffers: *ticket identifies the
@@ -186,10 +187,17 @@ int l5dh_comm_destroy(l5dh_ctx* ctx);
  * int32 counts [S][1798] and int64 totals [S] are summed with one RCCL
  * reduce-scatter (or all-reduce), and the rank summarizes the rows it received:
  * series [*first, *first + *count) (reduce-scatter: slice r of ceil(S/nranks)
- * rows; all-reduce: all S).  out (nullable) receives *count l5dh_summary,
+ * rows; all-reduce: all S).  The reduce-scatter moves the rows sparse: each rank
+ * sends each other rank the non-empty buckets of that rank's slice (one u32 per
+ * bucket: bucket << 21 | count; larger counts take a second word) and the words per
+ * row, and the totals go by one int64 reduce-scatter (l5dh_merge_bytes); the
+ * all-reduce moves them dense.  out (nullable) receives *count l5dh_summary,
  * counts_out / totals_out (nullable) the summed rows.  Each output must hold
  * ceil(S/nranks) rows (reduce-scatter) or S rows (all-reduce).  Integer sums:
- * bit-exact and independent of the reduction order. */
+ * bit-exact and independent of the reduction order.  The export consumes the
+ * rank's interval (as a resetting snapshot does) before the collective runs: if
+ * the collective then fails (-EIO, l5dh_last_error), that interval is lost -- the
+ * same outcome as a snapshot whose outputs are discarded. */
 int l5dh_merge(l5dh_ctx* ctx, int mode, l5dh_summary* out, int32_t* counts_out, int64_t* totals_out,
                uint32_t* first, uint32_t* count);
 /* The same for all contexts of an l5dh_comm_init_all communicator, from one
@@ -198,7 +206,14 @@ int l5dh_merge(l5dh_ctx* ctx, int mode, l5dh_summary* out, int32_t* counts_out, 
 int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_t** counts_outs,
                    int64_t** totals_outs, uint32_t* firsts, uint32_t* counts);
 
-/* Bin staged samples, wait for queued work; returns a deferred ingest error if any. */
+/* Bytes of the last l5dh_merge / l5dh_merge_all on this context (any pointer nullable):
+ * *dense = the dense rows + totals a reduce-scatter would move ([S][1798] int32 +
+ * [S] int64), *encoded = this rank's sparse encoding of them (non-empty buckets,
+ * words per row, totals), *sent = what it sent to the other ranks. */
+int l5dh_merge_bytes(l5dh_ctx* ctx, uint64_t* dense, uint64_t* encoded, uint64_t* sent);
+
+/* Bin staged samples, wait for queued work; returns -EINVAL (once) if the device
+ * found invalid series ids in any batch ingested since the last such report. */
 int l5dh_sync(l5dh_ctx* ctx);
 /* Run the context's work on an external hipStream_t, e.g. the caller's current
  * stream (torch's), so the context's kernels are ordered with the caller's work

@@ -72,10 +72,11 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
 
     private[this] def flushLocked(waitAll: Boolean): Unit = {
       if (n > 0) {
-        val t = Native.ingestAsync(ctx, ids(cur), values(cur), n)
-        check(t, "l5dh_ingest_async")
+        val m = n
+        n = 0 // cleared first: a batch the library refused is dropped, never re-sent (no double count)
+        val t = Native.ingestAsync(ctx, ids(cur), values(cur), m)
+        check(t, "l5dh_ingest_async") // < 0: this batch was not queued (deferred id errors come from sync)
         ticket(cur) = t
-        n = 0
         cur ^= 1
         // the other pair is refilled next: its copy must be done
         if (ticket(cur) != 0) { check(Native.ingestWait(ctx, ticket(cur)), "l5dh_ingest_wait"); ticket(cur) = 0 }
@@ -84,6 +85,12 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
         check(Native.ingestWait(ctx, ticket(k)), "l5dh_ingest_wait")
         ticket(k) = 0
       }
+    }
+
+    /** After a final flush: the pinned buffers go back to the library. */
+    def free(): Unit = synchronized {
+      flushLocked(waitAll = true)
+      for (b <- ids ++ values) Native.pinFree(b)
     }
   }
 
@@ -168,7 +175,13 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     }
   }
 
-  def close(): Unit = { flush(); check(Native.close(ctx), "l5dh_close") }
+  def close(): Unit = {
+    val it = stagings.iterator
+    while (it.hasNext) it.next.free() // every thread's staging: flushed, then its pinned buffers freed
+    stagings.clear()
+    check(Native.sync(ctx), "l5dh_sync")
+    check(Native.close(ctx), "l5dh_close")
+  }
 }
 
 /**
@@ -186,8 +199,13 @@ final class GpuStat(engine: GpuEngine) {
   def seriesId: Int = id
   def startingAt: Time = resetTime
 
-  /** A pruned Stat still accepts samples; they go nowhere (no exporter reads it). */
-  def add(value: Float): Unit = { val i = id; if (i >= 0) engine.add(i, value) }
+  /**
+   * A pruned Stat still accepts samples; they go nowhere (no exporter reads it).  The
+   * id is read and the sample staged under this Stat's monitor (Metric.scala:30-33 holds
+   * one per Stat), and `release` takes the id away under the same monitor: once it has,
+   * no add can stage the old id, which the engine may hand to a new Stat.
+   */
+  def add(value: Float): Unit = synchronized { val i = id; if (i >= 0) engine.add(i, value) }
 
   def peek: Seq[BucketAndCount] = { val i = id; if (i >= 0) engine.peek(i) else Nil }
 

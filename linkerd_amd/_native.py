@@ -30,14 +30,13 @@ PARAM_TIMING = 1
 PARAM_COLD_LIMIT = 2
 PARAM_HOT_CHUNK = 3
 PARAM_MAX_SEGMENTS = 4
-PARAM_BIN_MODE = 5
 PARAM_DIRECT_MAX = 6
 PARAM_DIRECT_DIV = 7
-PARAM_SPLIT_MIN = 8
 PARAM_STAGE_SAMPLES = 9
 PARAM_MAX_SLABS = 10
 PARAM_MERGE_RCCL_1RANK = 11
 PARAM_VARIANT = 12
+PARAM_REGION_PCT = 13
 
 MERGE_REDUCE_SCATTER = 0
 MERGE_ALL_REDUCE = 1
@@ -91,6 +90,7 @@ SIGNATURES = {
     "l5dh_comm_init_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int]),
     "l5dh_comm_destroy": (_c.c_int, [_vp]),
     "l5dh_merge": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
+    "l5dh_merge_bytes": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
     "l5dh_merge_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.POINTER(_vp), _c.POINTER(_vp),
                                   _c.POINTER(_vp), _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
 }

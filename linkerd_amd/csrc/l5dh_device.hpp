@@ -81,6 +81,10 @@ struct SrcLds16 {  // u16-packed row in LDS (cold tile: counts of the new record
     return make_uint4(w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16);
   }
 };
+struct SrcLds32 {  // u32 row in LDS, stride ROW, bins 1798/1799 zero
+  const uint32_t* row;
+  __device__ __forceinline__ uint4 get4(int b0) const { return *reinterpret_cast<const uint4*>(row + b0); }
+};
 struct SrcRow32 {  // state row, stride ROW = 1800 u32, 16-B aligned
   const uint32_t* row;
   __device__ __forceinline__ uint4 get4(int b0) const {
@@ -414,7 +418,8 @@ __device__ __forceinline__ uint32_t payload1_slow(uint32_t s, float f, Tables tb
   int64_t c;
   const uint32_t b = bucketize(f, tb.lut, tb.lim_pad, c);
   if (c >= 0 && c < (int64_t)V_ESC) return (uint32_t)c;  // e.g. f in (-1, 0) truncates to 0
-  atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)c);  // whole contribution
+  // whole contribution (nullptr: a redo pass of the same samples, already added)
+  if (sumfix) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)c);
   return V_ESC + b;
 }
 

@@ -23,6 +23,7 @@
 
 #include "../../include/l5dhist.h"
 #include "l5dh_kernels.hpp"
+#include "l5dh_merge.hpp"
 
 using namespace l5dh;
 
@@ -174,43 +175,29 @@ struct l5dh_ctx {
   uint8_t* d_dirty = nullptr;
   uint32_t* d_err = nullptr;
   // scratch
-  uint32_t* d_table = nullptr;  // [512][F + COLS] (G_max <= 512 slabs)
-  uint32_t* d_tile_tot = nullptr;  // [F + COLS] column totals (ingest), tile totals (snapshot plan)
+  uint32_t* d_tile_tot = nullptr;  // [F] tile totals (snapshot plan)
   uint32_t* d_cold_tile = nullptr;
-  DevBuf hot_item;    // big-tile chunk items (sized per snapshot)
-  DevBuf split_item;  // split-tile half chunk items (sized per snapshot)
+  DevBuf split_item;  // big-tile half chunk items (sized per snapshot)
   uint32_t* d_hot_list = nullptr;
   uint8_t* d_tile_flags = nullptr;
-  uint32_t* d_nosplit = nullptr;  // empty split set [SPLIT_SLOT] (single-level batches)
-  int split_cur = 0;              // split-set slot of the next batch in d_b2plan + PLAN_SPLIT
   uint32_t* d_header = nullptr;
-  uint32_t* d_b2plan = nullptr;  // ingest plan [PLAN_WORDS] (k_stplan)
-  uint32_t* h_header = nullptr;  // pinned: [0..3] plan header, [4] ingest error flag
-  uint32_t* h_header_dev = nullptr;  // its device-side address (the plan kernel writes the header there)
+  uint32_t* h_header = nullptr;      // pinned: [4] ingest error count (written by k_rfix1)
+  uint32_t* h_header_dev = nullptr;  // its device-side address
+  uint32_t* d_kest = nullptr;   // [2F] sampled ids per (tile, half) key of the batch being binned
+  uint32_t* d_kprev = nullptr;  // [2F] exact records per key of the previous batch (region sizes)
   int G_max = 256;
-  // segments
+  // segments: binned batches awaiting the snapshot
   struct Seg {
-    DevBuf recs;
-    uint32_t* tbase = nullptr;
-    uint32_t* sinfo = nullptr;  // [sinfo_words(F)] split tiles of the batch and their half-0 records
+    DevBuf rec32, rec16;
+    uint32_t* meta = nullptr;  // [meta_layout(F).words()]
     size_t n = 0;
   };
   Seg segs[MAX_SEG];
   int nseg = 0;
   int max_seg = 4;
-  // staging
-  DevBuf scratch1;  // level-1 records of the two-level partition
-  // paged ingest (bin mode 3): page pools, allocation logs, last pages, directory, level-2 counts
-  DevBuf pool, plog, tailpg, pdir, cnt2;
-  uint32_t* d_nlog = nullptr;   // [512] log entries per slab
-  uint32_t* d_pd = nullptr;     // [PD_WORDS]
-  uint32_t* d_ptot = nullptr;   // [F] tile totals of the paged final layout
-  uint32_t* d_pcount = nullptr; // [F] sampled ids per tile (k_psample; zeroed by k_pselect)
-  int bin_mode = 0;  // 0 auto, 1 single-level scatter, 2 two-level, 3 paged two-level
-  uint32_t direct_max = DIRECT_MAX;  // tiles k_bin1 may write in final form (0: none)
-  int dbg = 0;                       // L5DH_DBG: timing-only kernel variants (results invalid)
-  uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K sub-chunk
-  uint32_t split_min = 32768;        // split tiles (laid out per half-tile) have >= split_min records
+  uint32_t direct_max = DIRECT_MAX;  // direct tiles per batch (0: none)
+  uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K samples
+  uint32_t region_pct = 100;         // region capacity scale (L5DH_PARAM_REGION_PCT)
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // staging ring: small ingest batches are concatenated on the device and binned together
   DevBuf ring_series, ring_values;
@@ -228,8 +215,13 @@ struct l5dh_ctx {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   DevBuf merge_counts, merge_totals, recv_counts, recv_totals;
-  bool rccl_1rank = false;
-  uint32_t variant = 0;  // L5DH_PARAM_VARIANT: result-preserving kernel variants (A/B timing)  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
+  // sparse reduce-scatter (l5dh_merge.hip): this rank's encoding, the received slices
+  DevBuf m_words, m_offs, m_enc, m_tmp, m_sizes, r_words, r_offs, r_enc;
+  size_t m_tmp_bytes = 0;
+  std::vector<uint64_t> m_to, m_from;  // words to / from every rank
+  uint64_t m_dense_bytes = 0, m_encoded_bytes = 0, m_sent_bytes = 0;
+  bool rccl_1rank = false;  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
+  uint32_t variant = 0;  // L5DH_PARAM_VARIANT: result-preserving kernel variants (A/B timing)
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
   uint32_t hot_chunk = 1u << 18;  // records per big-tile item (u32 LDS bins, one half-tile per workgroup)
@@ -359,17 +351,17 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot,   c->d_cold_tile,   static_cast<uint32_t*>(c->hot_item.p), static_cast<uint2*>(c->split_item.p),
-              c->d_hot_list, c->d_tile_flags, c->d_header, c->h_header_dev};
+  return Plan{c->d_tile_tot, c->d_cold_tile, static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags,
+              c->d_header};
 }
 
 Segs segs_view(l5dh_ctx* c) {
   Segs s{};
   s.n = c->nseg;
   for (int j = 0; j < c->nseg; ++j) {
-    s.recs[j] = static_cast<const uint32_t*>(c->segs[j].recs.p);
-    s.tbase[j] = c->segs[j].tbase;
-    s.sinfo[j] = c->segs[j].sinfo;
+    s.rec32[j] = static_cast<const uint32_t*>(c->segs[j].rec32.p);
+    s.rec16[j] = static_cast<const uint16_t*>(c->segs[j].rec16.p);
+    s.meta[j] = c->segs[j].meta;
   }
   return s;
 }
@@ -382,18 +374,13 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   size_t recs = 0;
   for (int j = 0; j < c->nseg; ++j) recs += c->segs[j].n;
   // big-tile items: hot_chunk records, fewer when the pending records would leave CUs
-  // idle (C1, one series of 1e7 samples: 39 items of 2^18 for 256 CUs; with items of
-  // >= 2 per CU the accumulate takes 0.048 instead of 0.090 ms, C3 unchanged)
+  // idle (>= 2 items per CU when the records allow)
   uint32_t hc = c->hot_chunk;
   {
     const size_t fill = recs / (2 * (size_t)std::max(1, c->num_cu));
     hc = (uint32_t)std::min<size_t>(hc, std::max<size_t>(16384, (fill + 1023) & ~(size_t)1023));
   }
-  {
-    int r = ensure(c, c->hot_item, (recs / hc + c->F + 1) * 4);
-    if (!r) r = ensure(c, c->split_item, (recs / hc + 2 * (size_t)c->F + 2) * 8);
-    if (r) return r;
-  }
+  if (int r = ensure(c, c->split_item, (recs / hc + 2 * (size_t)c->F + 2) * 8)) return r;
   Plan pl = plan(c);
   {
     KTimer kt(c, L5DH_K_SCAN);
@@ -401,53 +388,36 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   }
   // The accumulate kernels are persistent and read their item counts from the plan
   // header on the device, so no host round trip separates them from the plan: the
-  // launches get upper bounds (a hot tile holds > cold_limit records).
-  uint32_t cold_items = DEV_COUNT;
-  uint32_t hot = (uint32_t)std::min<size_t>(c->F, recs / ((size_t)c->cold_limit + 1));
-  uint32_t hot_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / hc + hot);
-  uint32_t split_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / hc + 2 * (size_t)hot);
-  if (c->dbg) {  // development builds: the timing variants take exact host counts
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // the plan kernel wrote h_header (mapped pinned memory)
-    cold_items = c->h_header[0];
-    hot = c->h_header[1];
-    hot_items = c->h_header[2];
-    split_items = c->h_header[3];
-  }
+  // launches get upper bounds (a big tile holds > cold_limit records).
+  const uint32_t hot = (uint32_t)std::min<size_t>(c->F, recs / ((size_t)c->cold_limit + 1));
+  const uint32_t split_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / hc + 2 * (size_t)hot);
   State st = state(c);
   Tables tb = tables(c);
   // a resetting snapshot of every series into dense rows: clean big tiles count
   // straight into their output rows (no copy of state rows in k_hot_finish)
-  const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S &&
-                         !(c->dbg & 0x8000000);
+  const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S;
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, hc, c->stream));
+    HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, c->stream));
   }
   {
-    // cold tiles on the side stream, concurrently with the hot tiles (disjoint
+    // cold tiles on the side stream, concurrently with the big tiles (disjoint
     // tiles and series; the side stream joins back before anything reads them)
     KTimer kt(c, L5DH_K_ACCUM);
-    const bool two = cold_items && (hot_items || split_items) && !(c->dbg & 0x10000);
-    if (two) {
+    if (split_items) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPCHK(c, launch_accum(sv, pl, cold_items, 0, st, tb, out, c->cold_limit, hc, final_mode, reset,
-                             direct_out, c->side));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
-      if (hot_items)
-        HIPCHK(c, launch_accum(sv, pl, 0, hot_items, st, tb, out, c->cold_limit, hc, final_mode, reset,
-                               direct_out, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
-      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
-      HIPCHK(c, launch_accum(sv, pl, cold_items, hot_items, st, tb, out, c->cold_limit, hc, final_mode,
-                             reset, direct_out, c->stream));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));
     }
   }
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, direct_out, hc, c->stream));
+    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, direct_out, c->stream));
   }
   c->nseg = 0;
   return 0;
@@ -458,9 +428,8 @@ int fold(l5dh_ctx* c) {
   return aggregate(c, 0, 0, none);
 }
 
-// Invalid series ids: k_count adds to the device counter d_err (never reset);
-// every binned batch is followed by an asynchronous copy of it into pinned
-// h_header[4].  The host value only grows, so comparing it with the number of
+// Invalid series ids: k_rbin1 (k_fold1) adds to the device counter d_err (never
+// reset); k_rfix1 (a copy, after k_fold1) puts it into the pinned, mapped h_header[4].  The host value only grows, so comparing it with the number of
 // reports already returned needs no synchronization.
 int check_err(l5dh_ctx* c) {
   const uint32_t seen = __atomic_load_n(c->h_header + 4, __ATOMIC_ACQUIRE);
@@ -490,19 +459,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     ds = static_cast<const uint32_t*>(c->stage_series.p);
     dv = static_cast<const float*>(c->stage_values.p);
   }
-  auto& sg = c->segs[c->nseg];
-  {
-    int r = ensure(c, sg.recs, n * 4 + 64);  // readers load whole 16-B groups
-    if (r) return r;
-  }
-  // slabs: one workgroup per CU at most, >= 8K samples each, 16-B aligned starts
-  int G = (int)std::min<size_t>((size_t)c->G_max, (n + 8191) / 8192);
-  if (G < 1) G = 1;
-  size_t per = (n + G - 1) / G;
-  per = (per + 3) & ~(size_t)3;
-  G = (int)((n + per - 1) / per);
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
-  if (c->F == 1 && !(c->variant & 12)) {  // one tile: fold the batch into its state rows now
+  if (c->F == 1) {  // one tile: fold the batch into its state rows now (no records, no segment)
     KTimer kt(c, L5DH_K_BIN);
     const size_t fill = n / (2 * (size_t)std::max(1, c->num_cu));  // >= 2 items per CU when the batch allows
     const uint32_t chunk =
@@ -511,127 +469,67 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     return 0;
   }
-  if (c->F == 1 && !(c->variant & 4)) {  // (variant bit 3) one tile: the samples in input order are its records
-    {
-      KTimer kt(c, L5DH_K_BIN);
-      HIPCHK(c, launch_encode1(ds, dv, n, c->S, tables(c), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, sg.tbase,
-                               c->d_err, vec, c->num_cu, c->stream));
-      HIPCHK(c, launch_seginfo(c->d_nosplit, c->d_tile_tot, c->F, sg.sinfo, c->stream));
-    }
-    sg.n = n;
-    c->nseg++;
-    HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-    return 0;
-  }
-  if (c->bin_mode == 3) {  // paged: no counting pass (l5dh_paged.hip)
-    const size_t pp = paged_pool_pages(per);
-    if ((double)G * (double)pp * PAGE >= 4294967296.0) return fail(c, -EINVAL, "paged ingest: batch too large");
-    int r = ensure(c, c->pool, (size_t)G * pp * PAGE * 4);
-    if (!r) r = ensure(c, c->plog, (size_t)G * pp * 8);
-    if (!r) r = ensure(c, c->tailpg, (size_t)G * PG_BINS * 8);
-    if (!r) r = ensure(c, c->pdir, (size_t)G * pp * 8);
-    if (!r) r = ensure(c, c->cnt2, ((size_t)G * pp / KP + 1024) * 64 * 4);
-    if (r) return r;
-    const uint32_t FS = (c->F + 63) / 64;
-    PagedArgs a{};
-    a.series = ds;
-    a.values = dv;
-    a.n = n;
-    a.per = per;
-    a.G = G;
-    a.num_cu = c->num_cu;
-    a.S = c->S;
-    a.F = c->F;
-    a.plan = c->d_b2plan;
-    a.tb = tables(c);
-    a.state = state(c);
-    a.err = c->d_err;
-    a.pool_pages = (uint32_t)pp;
-    a.pool = static_cast<uint32_t*>(c->pool.p);
-    a.plog = static_cast<uint2*>(c->plog.p);
-    a.nlog = c->d_nlog;
-    a.tailpg = static_cast<uint2*>(c->tailpg.p);
-    a.pd = c->d_pd;
-    a.dir = static_cast<uint2*>(c->pdir.p);
-    a.cnt2 = static_cast<uint32_t*>(c->cnt2.p);
-    a.tot = c->d_ptot;
-    a.pcount = c->d_pcount;
-    a.err_host = c->h_header_dev + 4;
-    a.tile_base = sg.tbase;
-    a.records = static_cast<uint32_t*>(sg.recs.p);
-    a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
-    a.dmax = std::min<uint32_t>(c->direct_max, std::min<uint32_t>(DIRECT_MAX, ((uint32_t)PG_BINS - 1 - FS) / 2));
-    a.vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
-    {
-      KTimer kt(c, L5DH_K_BIN);
-      HIPCHK(c, launch_paged_ingest(a, 0, c->stream));
-    }
-    {
-      KTimer kt(c, L5DH_K_SCAN);
-      HIPCHK(c, launch_paged_ingest(a, 1, c->stream));
-      HIPCHK(c, launch_seginfo(c->d_nosplit, c->d_tile_tot, c->F, sg.sinfo, c->stream));
-    }
-    {
-      KTimer kt(c, L5DH_K_HOT);
-      HIPCHK(c, launch_paged_ingest(a, 2, c->stream));
-    }
-    {
-      KTimer kt(c, L5DH_K_BIN2);
-      HIPCHK(c, launch_paged_ingest(a, 3, c->stream));
-    }
-    sg.n = n;
-    c->nseg++;
-    return 0;  // (k_p2scan_b wrote the invalid-id count to h_header[4])
-  }
-  const bool two_level = c->bin_mode != 1;
-  // split set of this batch (chosen from the previous batch's tile totals) and of the next
-  uint32_t* split_slot = c->d_b2plan + PLAN_SPLIT;
-  const uint32_t* cur = two_level ? split_slot + c->split_cur * SPLIT_SLOT : c->d_nosplit;
-  uint32_t* nxt = split_slot + (c->split_cur ^ 1) * SPLIT_SLOT;
+  auto& sg = c->segs[c->nseg];
+  // region buffers: the plan sizes the regions from the previous batch and a sample
+  // of this one, with slack; a plan that does not fit is scaled to these sizes (an
+  // overflowing region is then redone with exact sizes, which always fit)
+  const size_t cap32 = n + n / 4 + ((size_t)1 << 19);
+  const size_t cap16 = n + n / 4 + (size_t)64 * 2 * c->F;
   {
-    KTimer kt(c, L5DH_K_COUNT);
-    HIPCHK(c, launch_count(ds, n, per, G, c->S, c->F, c->d_table, c->d_err, c->d_b2plan + PLAN_HINT, cur, vec,
-                           c->stream));
+    int r = ensure(c, sg.rec32, (cap32 + 16) * 4);  // readers load whole 16-B groups
+    if (!r) r = ensure(c, sg.rec16, (cap16 + 16) * 2);
+    if (r) return r;
+  }
+  // slabs: one workgroup per CU at most, >= 8K samples each, 16-B aligned starts
+  int G = (int)std::min<size_t>((size_t)c->G_max, (n + 8191) / 8192);
+  if (G < 1) G = 1;
+  size_t per = (n + G - 1) / G;
+  per = (per + 3) & ~(size_t)3;
+  G = (int)((n + per - 1) / per);
+  IngestArgs a{};
+  a.series = ds;
+  a.values = dv;
+  a.n = n;
+  a.per = per;
+  a.G = G;
+  a.num_cu = c->num_cu;
+  a.S = c->S;
+  a.F = c->F;
+  a.tb = tables(c);
+  a.sumfix = c->d_sumfix;
+  a.err = c->d_err;
+  a.err_host = c->h_header_dev + 4;
+  a.kest = c->d_kest;
+  a.kprev = c->d_kprev;
+  a.meta = sg.meta;
+  a.rec32 = static_cast<uint32_t*>(sg.rec32.p);
+  a.rec16 = static_cast<uint16_t*>(sg.rec16.p);
+  a.cap32 = cap32;
+  a.cap16 = cap16;
+  a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
+  const uint32_t FS = (c->F + 63) / 64;
+  a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + the trash bin
+  a.pct = c->region_pct;
+  a.vec = vec;
+  {
+    KTimer kt(c, L5DH_K_SCAN);
+    HIPCHK(c, launch_ingest(a, 0, c->stream));
+  }
+  {
+    KTimer kt(c, L5DH_K_BIN);
+    HIPCHK(c, launch_ingest(a, 1, c->stream));
   }
   {
     KTimer kt(c, L5DH_K_SCAN);
-    HIPCHK(c, launch_colscan(c->d_table, G, c->F, c->d_tile_tot, c->stream));
-    HIPCHK(c, launch_tilescan_seg(c->d_tile_tot, c->F, cur, sg.tbase, sg.sinfo, c->stream));
+    HIPCHK(c, launch_ingest(a, 2, c->stream));
   }
-  if (two_level) {
-    int r = ensure(c, c->scratch1, (n + BIN1_SCRATCH_PAD) * 4);  // trash bin; k_bin2 reads whole 16-B groups
-    if (r) return r;
-    {
-      KTimer kt(c, L5DH_K_SCAN);
-      const uint64_t thr_min = std::max<uint64_t>(1, n / (8192ull * c->direct_div));
-      HIPCHK(c, launch_stplan(c->F, G, c->d_tile_tot, c->d_b2plan, cur, nxt,
-                              (uint32_t)std::min<uint64_t>(thr_min, 0xFFFFFFFFull), c->direct_max, c->split_min,
-                              // the hot k_bin1 bins (ballot ranking when one holds >= half); all 8
-                              // for the lane-private-slot development variant (L5DH_DBG bit 22)
-                              1 | (((c->dbg >> 22) & 1) ? 4 : 0),
-                              c->d_err, c->h_header_dev + 4, c->stream));
-      c->split_cur ^= 1;
-    }
-    {
-      KTimer kt(c, L5DH_K_BIN);
-      HIPCHK(c, launch_bin1(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c), c->d_b2plan,
-                            c->d_tile_tot, cur, static_cast<uint32_t*>(c->scratch1.p), static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec,
-                            c->dbg | (int)(c->variant << 27), c->stream));
-    }
+  {
     KTimer kt(c, L5DH_K_BIN2);
-    HIPCHK(c, launch_bin2(static_cast<uint32_t*>(c->scratch1.p), n, G, c->F, c->d_table, sg.tbase, c->d_tile_tot,
-                          cur, tables(c), c->d_b2plan, static_cast<uint32_t*>(sg.recs.p), c->dbg, c->stream));
-  } else {
-    KTimer kt(c, L5DH_K_BIN);
-    HIPCHK(c, launch_bin(ds, dv, n, per, G, c->S, c->F, c->d_table, sg.tbase, tables(c),
-                         static_cast<uint32_t*>(sg.recs.p), c->d_sumfix, vec, c->stream));
+    HIPCHK(c, launch_ingest(a, 3, c->stream));
   }
   sg.n = n;
   c->nseg++;
-  // the invalid-id counter follows the batch to the host asynchronously (check_err):
-  // k_stplan writes it to the mapped pinned word; the single-level path copies it
-  if (!two_level) HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
-  return 0;
+  return 0;  // (k_rfix1 wrote the invalid-id count to h_header[4])
 }
 
 // Bin the staging ring as one batch.
@@ -793,36 +691,118 @@ int merge_export(l5dh_ctx* c) {
   return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot});
 }
 
-// Phase 2: the collective (callers group it across contexts).
+// Phase 2 (reduce-scatter): the rows are exchanged sparse (l5dh_merge.hip) -- per
+// destination rank, the non-empty buckets of its slice plus the words per row --
+// and the totals by one int64 reduce-scatter.  A 1-rank communicator skips it (an
+// identity) unless L5DH_PARAM_MERGE_RCCL_1RANK forces it, with the encoding sent to
+// itself through RCCL.  Steps: encode (local, one host wait for the slice sizes),
+// sizes (collective: an all-gather of the words-to matrix), receive buffers (local,
+// one host wait), payload (collective).  l5dh_merge_all groups each collective step
+// over its contexts.
 bool merge_skips_collective(const l5dh_ctx* c) { return c->nranks == 1 && !c->rccl_1rank; }
 
-int merge_collective(l5dh_ctx* c, int mode) {
-  if (merge_skips_collective(c)) return 0;  // one rank: the sum is the identity
-  const size_t per = merge_per(c);
+int merge_encode_step(l5dh_ctx* c) {
+  const uint32_t per = merge_per(c);
+  const uint32_t Sp = per * (uint32_t)c->nranks;
+  const int W = c->nranks;
+  int r;
   KTimer kt(c, L5DH_K_MERGE);
-  if (mode == L5DH_MERGE_REDUCE_SCATTER) {
-    int r;
-    if ((r = ensure(c, c->recv_counts, per * NB * 4)) || (r = ensure(c, c->recv_totals, per * 8))) return r;
-    NCCLCHK(c, ncclReduceScatter(c->merge_counts.p, c->recv_counts.p, per * NB, ncclInt32, ncclSum, c->comm, c->stream));
-    NCCLCHK(c, ncclReduceScatter(c->merge_totals.p, c->recv_totals.p, per, ncclInt64, ncclSum, c->comm, c->stream));
-  } else {
-    const size_t Sp = per * c->nranks;
-    NCCLCHK(c, ncclAllReduce(c->merge_counts.p, c->merge_counts.p, Sp * NB, ncclInt32, ncclSum, c->comm, c->stream));
-    NCCLCHK(c, ncclAllReduce(c->merge_totals.p, c->merge_totals.p, Sp, ncclInt64, ncclSum, c->comm, c->stream));
-  }
+  c->m_tmp_bytes = 0;  // (the scans of every slice fit the storage of this, the longest one)
+  HIPCHK(c, merge_count(nullptr, Sp, nullptr, nullptr, nullptr, &c->m_tmp_bytes, c->stream));
+  if ((r = ensure(c, c->m_words, ((size_t)Sp + 1) * 4)) || (r = ensure(c, c->m_offs, ((size_t)Sp + 1) * 8)) ||
+      (r = ensure(c, c->m_tmp, c->m_tmp_bytes)) || (r = ensure(c, c->m_sizes, (size_t)W * W * 8)))
+    return r;
+  uint32_t* words = static_cast<uint32_t*>(c->m_words.p);
+  uint64_t* offs = static_cast<uint64_t*>(c->m_offs.p);
+  HIPCHK(c, merge_count(static_cast<const int32_t*>(c->merge_counts.p), Sp, words, offs, c->m_tmp.p, &c->m_tmp_bytes,
+                        c->stream));
+  std::vector<uint64_t> bnd(W + 1);
+  for (int q = 0; q <= W; ++q)
+    HIPCHK(c, hipMemcpyAsync(&bnd[q], offs + (size_t)q * per, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((r = ensure(c, c->m_enc, (size_t)bnd[W] * 4 + 16))) return r;
+  HIPCHK(c, merge_encode(static_cast<const int32_t*>(c->merge_counts.p), Sp, offs, static_cast<uint32_t*>(c->m_enc.p),
+                         c->stream));
+  c->m_to.assign(W, 0);
+  for (int q = 0; q < W; ++q) c->m_to[q] = bnd[q + 1] - bnd[q];
+  c->m_dense_bytes = (uint64_t)Sp * (NB * 4 + 8);
+  c->m_encoded_bytes = bnd[W] * 4 + (uint64_t)Sp * (4 + 8);  // entries + words per row + totals
+  // this rank's row of the size matrix, for the all-gather
+  HIPCHK(c, hipMemcpyAsync(static_cast<uint64_t*>(c->m_sizes.p) + (size_t)c->rank * W, c->m_to.data(), (size_t)W * 8,
+                           hipMemcpyHostToDevice, c->stream));
   return 0;
 }
 
-// Phase 3: summaries (+ copies) of the rows this rank received.
+int merge_sizes_step(l5dh_ctx* c) {
+  const int W = c->nranks;
+  uint64_t* m = static_cast<uint64_t*>(c->m_sizes.p);
+  NCCLCHK(c, ncclAllGather(m + (size_t)c->rank * W, m, (size_t)W, ncclUint64, c->comm, c->stream));
+  return 0;
+}
+
+int merge_recv_step(l5dh_ctx* c) {
+  const uint32_t per = merge_per(c);
+  const int W = c->nranks;
+  std::vector<uint64_t> mat((size_t)W * W);
+  HIPCHK(c, hipMemcpyAsync(mat.data(), c->m_sizes.p, mat.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->m_from.assign(W, 0);
+  uint64_t all = 0;
+  for (int s = 0; s < W; ++s) all += (c->m_from[s] = mat[(size_t)s * W + c->rank]);
+  int r;
+  if ((r = ensure(c, c->r_enc, (size_t)all * 4 + 16)) || (r = ensure(c, c->r_words, (size_t)W * per * 4)) ||
+      (r = ensure(c, c->r_offs, (size_t)W * per * 8)) || (r = ensure(c, c->recv_totals, (size_t)per * 8)))
+    return r;
+  uint64_t sent = 0;
+  for (int q = 0; q < W; ++q)
+    if (q != c->rank) sent += 4 * c->m_to[q] + 4ull * per + 8ull * per;
+  c->m_sent_bytes = sent;
+  return 0;
+}
+
+int merge_payload_step(l5dh_ctx* c) {
+  const uint32_t per = merge_per(c);
+  const int W = c->nranks;
+  const uint32_t* enc = static_cast<const uint32_t*>(c->m_enc.p);
+  const uint32_t* words = static_cast<const uint32_t*>(c->m_words.p);
+  uint32_t* renc = static_cast<uint32_t*>(c->r_enc.p);
+  uint32_t* rwords = static_cast<uint32_t*>(c->r_words.p);
+  KTimer kt(c, L5DH_K_MERGE);
+  uint64_t at = 0, rat = 0;
+  for (int q = 0; q < W; ++q) {
+    // (the local slice is read in place, except in a forced 1-rank exchange)
+    if (q != c->rank || W == 1) {
+      if (c->m_to[q]) NCCLCHK(c, ncclSend(enc + at, c->m_to[q], ncclUint32, q, c->comm, c->stream));
+      NCCLCHK(c, ncclSend(words + (size_t)q * per, per, ncclUint32, q, c->comm, c->stream));
+      if (c->m_from[q]) NCCLCHK(c, ncclRecv(renc + rat, c->m_from[q], ncclUint32, q, c->comm, c->stream));
+      NCCLCHK(c, ncclRecv(rwords + (size_t)q * per, per, ncclUint32, q, c->comm, c->stream));
+    }
+    at += c->m_to[q];
+    rat += c->m_from[q];
+  }
+  NCCLCHK(c, ncclReduceScatter(c->merge_totals.p, c->recv_totals.p, per, ncclInt64, ncclSum, c->comm, c->stream));
+  return 0;
+}
+
+int merge_dense_allreduce(l5dh_ctx* c) {
+  const size_t Sp = (size_t)merge_per(c) * c->nranks;
+  KTimer kt(c, L5DH_K_MERGE);
+  c->m_dense_bytes = c->m_encoded_bytes = Sp * (NB * 4 + 8);
+  c->m_sent_bytes = c->nranks > 1 ? 2 * c->m_dense_bytes * (c->nranks - 1) / c->nranks : 0;
+  NCCLCHK(c, ncclAllReduce(c->merge_counts.p, c->merge_counts.p, Sp * NB, ncclInt32, ncclSum, c->comm, c->stream));
+  NCCLCHK(c, ncclAllReduce(c->merge_totals.p, c->merge_totals.p, Sp, ncclInt64, ncclSum, c->comm, c->stream));
+  return 0;
+}
+
+// Phase 3: the rows this rank receives -- decoded from every source and summarized
+// (reduce-scatter), or the all-reduced dense rows summarized -- and the copies.
 int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, int64_t* totals_out, uint32_t* first,
                  uint32_t* count) {
   const uint32_t per = merge_per(c);
   const bool rs = mode == L5DH_MERGE_REDUCE_SCATTER;
-  const bool recv = rs && !merge_skips_collective(c);
+  const bool sparse = rs && !merge_skips_collective(c);
   const uint32_t f = rs ? (uint32_t)std::min<uint64_t>((uint64_t)c->rank * per, c->S) : 0u;
   const uint32_t n = rs ? std::min<uint32_t>(per, c->S - f) : c->S;
-  const int32_t* rows = static_cast<const int32_t*>(recv ? c->recv_counts.p : c->merge_counts.p);
-  const int64_t* tots = static_cast<const int64_t*>(recv ? c->recv_totals.p : c->merge_totals.p);
   if (first) *first = f;
   if (count) *count = n;
   if (n == 0) return sync_stream(c);
@@ -836,6 +816,58 @@ int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, 
       if ((r = ensure(c, c->stage_summ, (size_t)n * 88))) return r;
       d_summ = static_cast<Summary88*>(c->stage_summ.p);
     }
+  }
+  const int32_t* rows = static_cast<const int32_t*>(c->merge_counts.p);
+  const int64_t* tots = static_cast<const int64_t*>(c->merge_totals.p);
+  if (sparse) {
+    const int W = c->nranks;
+    if (W > MERGE_MAX_RANKS) return fail(c, -EINVAL, "fleet merge: more than 64 ranks");
+    const bool cnt_dev = counts_out && is_device_ptr(counts_out) && ((uintptr_t)counts_out % 8 == 0);
+    int32_t* drows = nullptr;
+    if (counts_out) {
+      if (cnt_dev)
+        drows = counts_out;
+      else {
+        if ((r = ensure(c, c->recv_counts, (size_t)per * NB * 4))) return r;
+        drows = static_cast<int32_t*>(c->recv_counts.p);
+      }
+    }
+    MergeSources src{};
+    src.n = W;
+    uint64_t rat = 0;
+    KTimer kt(c, L5DH_K_MERGE);
+    for (int q = 0; q < W; ++q) {
+      const bool local = q == c->rank && W > 1;
+      if (local) {  // this rank's own slice, in place
+        uint64_t a0 = 0;
+        for (int k = 0; k < q; ++k) a0 += c->m_to[k];
+        src.enc[q] = static_cast<const uint32_t*>(c->m_enc.p) + a0;
+        src.words[q] = static_cast<const uint32_t*>(c->m_words.p) + (size_t)q * per;
+      } else {
+        src.enc[q] = static_cast<const uint32_t*>(c->r_enc.p) + rat;
+        src.words[q] = static_cast<const uint32_t*>(c->r_words.p) + (size_t)q * per;
+      }
+      uint64_t* o = static_cast<uint64_t*>(c->r_offs.p) + (size_t)q * per;
+      HIPCHK(c, merge_offsets(src.words[q], per, o, c->m_tmp.p, c->m_tmp_bytes, c->stream));
+      src.offs[q] = o;
+      rat += c->m_from[q];
+    }
+    HIPCHK(c, merge_decode(src, n, static_cast<const int64_t*>(c->recv_totals.p), tables(c), drows, d_summ, c->stream));
+    rows = drows;
+    tots = static_cast<const int64_t*>(c->recv_totals.p);
+    KTimer kc(c, L5DH_K_COPY);
+    if (out && !out_dev) HIPCHK(c, hipMemcpyAsync(out, d_summ, (size_t)n * 88, hipMemcpyDefault, c->stream));
+    if (counts_out && !cnt_dev)
+      HIPCHK(c, hipMemcpyAsync(counts_out, rows, (size_t)n * NB * 4, hipMemcpyDefault, c->stream));
+    if (totals_out) HIPCHK(c, hipMemcpyAsync(totals_out, tots, (size_t)n * 8, hipMemcpyDefault, c->stream));
+    return sync_stream(c);
+  }
+  if (rs) {  // a 1-rank communicator, collective skipped: the exported rows are the sums
+    c->m_dense_bytes = (uint64_t)per * (NB * 4 + 8);
+    c->m_encoded_bytes = c->m_dense_bytes;
+    c->m_sent_bytes = 0;
+  }
+  if (out) {
     KTimer kt(c, L5DH_K_HOT);
     HIPCHK(c, launch_rows(state(c), rows, tots, tables(c), Outputs{d_summ, nullptr, 0, n, nullptr}, 0, nullptr,
                           c->stream));
@@ -847,6 +879,47 @@ int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, 
     if (totals_out) HIPCHK(c, hipMemcpyAsync(totals_out, tots, (size_t)n * 8, hipMemcpyDefault, c->stream));
   }
   return sync_stream(c);
+}
+
+// The collective steps of one merge over contexts `cs` (one, or every context of an
+// l5dh_comm_init_all communicator): each collective step is grouped over them.
+int merge_collectives(l5dh_ctx** cs, int n, int mode) {
+  int r = 0;
+  if (mode != L5DH_MERGE_REDUCE_SCATTER) {
+    NCCLCHK(cs[0], ncclGroupStart());
+    for (int i = 0; i < n && !r; ++i) {
+      hipSetDevice(cs[i]->device);
+      if (!merge_skips_collective(cs[i])) r = merge_dense_allreduce(cs[i]);
+    }
+    const ncclResult_t ge = ncclGroupEnd();
+    if (r) return r;
+    return ge == ncclSuccess ? 0 : ncclfail(cs[0], ge, "ncclGroupEnd");
+  }
+  if (merge_skips_collective(cs[0])) return 0;
+  for (int i = 0; i < n; ++i) {
+    hipSetDevice(cs[i]->device);
+    if ((r = merge_encode_step(cs[i]))) return r;
+  }
+  NCCLCHK(cs[0], ncclGroupStart());
+  for (int i = 0; i < n && !r; ++i) {
+    hipSetDevice(cs[i]->device);
+    r = merge_sizes_step(cs[i]);
+  }
+  ncclResult_t ge = ncclGroupEnd();
+  if (r) return r;
+  if (ge != ncclSuccess) return ncclfail(cs[0], ge, "ncclGroupEnd");
+  for (int i = 0; i < n; ++i) {
+    hipSetDevice(cs[i]->device);
+    if ((r = merge_recv_step(cs[i]))) return r;
+  }
+  NCCLCHK(cs[0], ncclGroupStart());
+  for (int i = 0; i < n && !r; ++i) {
+    hipSetDevice(cs[i]->device);
+    r = merge_payload_step(cs[i]);
+  }
+  ge = ncclGroupEnd();
+  if (r) return r;
+  return ge == ncclSuccess ? 0 : ncclfail(cs[0], ge, "ncclGroupEnd");
 }
 
 }  // namespace
@@ -881,10 +954,6 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   auto* c = new (std::nothrow) l5dh_ctx();
   if (!c) return -ENOMEM;
   c->device = dev;
-#ifdef L5DH_DEV
-  // development builds only (tools/mk_var.sh): timing-only kernel variants, results invalid
-  if (const char* d = getenv("L5DH_DBG")) c->dbg = atoi(d);
-#endif
   c->S = max_series;
   // staging ring: 64 samples per series, between 2^20 and 2^26 samples (4 MB .. 256 MB per array)
   c->ring_cap = std::min<size_t>(std::max<size_t>((size_t)max_series * 64, (size_t)1 << 20), (size_t)1 << 26);
@@ -896,14 +965,9 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   if (hipSetDevice(dev) != hipSuccess) return bail(-EIO);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) c->num_cu = prop.multiProcessorCount;
-  // one slab per CU: the count and level-1 kernels hold one 1024-thread workgroup per
-  // CU (LDS-bound), so a second round of slabs only adds table rows (measured: 2 x CUs
-  // is ~1.4 % slower on C2 and no faster on C3)
+  // one slab per CU: the level-1 kernel holds one 1024-thread workgroup per CU (LDS-bound)
   c->G_max = std::max(1, std::min(c->num_cu, 512));
-  if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess ||
-      set_paged_attributes() != hipSuccess)
-    return bail(-EIO);
-  if (c->dbg && set_snapshot_debug(c->dbg) != hipSuccess) return bail(-EIO);
+  if (set_ingest_attributes() != hipSuccess || set_snapshot_attributes() != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) return bail(-EIO);
   if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -916,20 +980,17 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
-            mal((void**)&c->d_err, 4) && mal((void**)&c->d_table, (size_t)512 * (F + COLS) * 4) &&
-            mal((void**)&c->d_tile_tot, (F + COLS) * 4) && mal((void**)&c->d_cold_tile, (F + 1) * 4) &&
-            mal((void**)&c->d_hot_list, F * 4) && mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) &&
-            mal((void**)&c->d_b2plan, 4 * PLAN_WORDS) && mal((void**)&c->d_tile_flags, F) &&
-            mal((void**)&c->d_nosplit, 4 * SPLIT_SLOT) && mal((void**)&c->d_nlog, 512 * 4) &&
-            mal((void**)&c->d_pd, 4 * PD_WORDS) && mal((void**)&c->d_ptot, F * 4) &&
-            mal((void**)&c->d_pcount, F * 4);
-  for (int j = 0; ok && j < MAX_SEG; ++j)
-    ok = mal((void**)&c->segs[j].tbase, (F + 1) * 4) && mal((void**)&c->segs[j].sinfo, sinfo_words(c->F) * 4);
+            mal((void**)&c->d_err, 4) && mal((void**)&c->d_tile_tot, F * 4) &&
+            mal((void**)&c->d_cold_tile, (F + 1) * 4) && mal((void**)&c->d_hot_list, F * 4) &&
+            mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) && mal((void**)&c->d_tile_flags, F) &&
+            mal((void**)&c->d_kest, 2 * F * 4) && mal((void**)&c->d_kprev, 2 * F * 4);
+  const size_t meta_bytes = (size_t)meta_layout((uint32_t)F).words() * 4;
+  for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].meta, meta_bytes);
   if (!ok) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
   }
-  if (hipHostMalloc((void**)&c->h_header, 32, hipHostMallocMapped) != hipSuccess) return bail(-ENOMEM);  // header[4] + err count
+  if (hipHostMalloc((void**)&c->h_header, 32, hipHostMallocMapped) != hipSuccess) return bail(-ENOMEM);  // [4]: err count
   memset(c->h_header, 0, 32);
   if (hipHostGetDevicePointer((void**)&c->h_header_dev, c->h_header, 0) != hipSuccess) return bail(-ENOMEM);
   // constant tables
@@ -950,13 +1011,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
       hipMemcpy(c->d_mid, mid, sizeof(mid), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_base, base, sizeof(base), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(c->d_dirty, 0, F) != hipSuccess || hipMemset(c->d_sumfix, 0, S * 8) != hipSuccess ||
-      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_b2plan, 0xFF, 4 * PLAN_SPLIT) != hipSuccess ||
-      hipMemset(c->d_b2plan + PLAN_SPLIT, 0, 4 * 2 * SPLIT_SLOT) != hipSuccess ||
-      // no direct tiles before the first batch (the paged path reads the previous batch's)
-      hipMemset(c->d_b2plan + PLAN_DBITS, 0, 4 * 2048) != hipSuccess ||
-      hipMemset(c->d_b2plan + PLAN_ND, 0, 4) != hipSuccess ||
-      hipMemset(c->d_nosplit, 0, 4 * SPLIT_SLOT) != hipSuccess || hipMemset(c->d_pcount, 0, F * 4) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess)
+      hipMemset(c->d_err, 0, 4) != hipSuccess || hipMemset(c->d_kest, 0, 2 * F * 4) != hipSuccess ||
+      hipMemset(c->d_kprev, 0, 2 * F * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return bail(-EIO);
   *out = c;
   return 0;
@@ -971,22 +1027,23 @@ int l5dh_close(l5dh_ctx* c) {
     hipEventDestroy(e.b);
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
-  void* ptrs[] = {c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->d_err,
-                  c->d_table, c->d_tile_tot, c->d_cold_tile, c->d_hot_list, c->d_header, c->d_b2plan, c->d_tile_flags, c->d_nosplit,
-                  c->d_nlog, c->d_pd, c->d_ptot, c->d_pcount};
+  void* ptrs[] = {c->d_lim_pad, c->d_mid,      c->d_base,     c->d_lut,       c->d_lut2,     c->d_counts,
+                  c->d_total,   c->d_sumfix,   c->d_dirty,    c->d_err,       c->d_tile_tot, c->d_cold_tile,
+                  c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
-    if (s.tbase) hipFree(s.tbase);
-    if (s.sinfo) hipFree(s.sinfo);
-    if (s.recs.p) hipFree(s.recs.p);
+    if (s.meta) hipFree(s.meta);
+    if (s.rec32.p) hipFree(s.rec32.p);
+    if (s.rec16.p) hipFree(s.rec16.p);
   }
   if (c->comm) ncclCommDestroy(c->comm);
-  DevBuf* bufs[] = {&c->scratch1,      &c->hot_item,        &c->split_item,   &c->stage_series, &c->stage_values,
-                    &c->stage_summ,    &c->stage_counts,    &c->stage_totals, &c->stage_in_counts,
-                    &c->stage_in_totals, &c->ring_series,   &c->ring_values,  &c->merge_counts,  &c->merge_totals,
-                    &c->recv_counts,   &c->recv_totals,     &c->pool,         &c->plog,         &c->tailpg,
-                    &c->pdir,          &c->cnt2};
+  DevBuf* bufs[] = {&c->split_item,      &c->stage_series, &c->stage_values,  &c->stage_summ,
+                    &c->stage_counts,    &c->stage_totals, &c->stage_in_counts, &c->stage_in_totals,
+                    &c->ring_series,     &c->ring_values,  &c->merge_counts,   &c->merge_totals,
+                    &c->recv_counts,     &c->recv_totals,  &c->m_words,        &c->m_offs,
+                    &c->m_enc,           &c->m_tmp,        &c->m_sizes,        &c->r_words,
+                    &c->r_offs,          &c->r_enc};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->h_header) hipHostFree(c->h_header);
@@ -1006,8 +1063,9 @@ int l5dh_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t
   if (n && (!series || !values)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  const int r = ingest_impl(c, series, values, n);
-  return r ? r : check_err(c);
+  // 0 = the batch was accepted; a deferred invalid-id report never rides on a later
+  // batch's status (l5dh_sync returns it), so a caller never re-sends an accepted batch
+  return ingest_impl(c, series, values, n);
 }
 
 int l5dh_ingest_async(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n, uint64_t* ticket) {
@@ -1015,8 +1073,7 @@ int l5dh_ingest_async(l5dh_ctx* c, const uint32_t* series, const float* values, 
   if (n && (!series || !values)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  const int r = ingest_impl(c, series, values, n, ticket);
-  return r ? r : check_err(c);
+  return ingest_impl(c, series, values, n, ticket);  // (deferred id errors: l5dh_sync)
 }
 
 int l5dh_ingest_wait(l5dh_ctx* c, uint64_t ticket) {
@@ -1199,10 +1256,6 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       }
       c->max_seg = (int)v;
       return 0;
-    case L5DH_PARAM_BIN_MODE:
-      if (v < 0 || v > 3) return fail(c, -EINVAL, "bin mode must be 0 (auto), 1 (single), 2 (two-level) or 3 (paged)");
-      c->bin_mode = (int)v;
-      return 0;
     case L5DH_PARAM_DIRECT_MAX:
       if (v < 0 || v > DIRECT_MAX) return fail(c, -EINVAL, "direct tiles must be in [0, 255]");
       c->direct_max = (uint32_t)v;
@@ -1210,10 +1263,6 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
     case L5DH_PARAM_DIRECT_DIV:
       if (v < 1 || v > 65536) return fail(c, -EINVAL, "direct divisor must be in [1, 65536]");
       c->direct_div = (uint32_t)v;
-      return 0;
-    case L5DH_PARAM_SPLIT_MIN:
-      if (v < 1 || v > 0xFFFFFFFFll) return fail(c, -EINVAL, "split minimum must be in [1, 2^32)");
-      c->split_min = (uint32_t)v;
       return 0;
     case L5DH_PARAM_STAGE_SAMPLES: {
       if (v < 0 || v > (int64_t)MAX_BATCH) return fail(c, -EINVAL, "staging ring must be in [0, 2^30 - 65536] samples");
@@ -1232,8 +1281,12 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       return 0;
     }
     case L5DH_PARAM_VARIANT:
-      if (v < 0 || v > 15) return fail(c, -EINVAL, "variant bits must be in [0, 15]");
+      if (v < 0 || v > 3) return fail(c, -EINVAL, "variant bits must be in [0, 3]");
       c->variant = (uint32_t)v;
+      return 0;
+    case L5DH_PARAM_REGION_PCT:
+      if (v < 1 || v > 1000) return fail(c, -EINVAL, "region capacity percent must be in [1, 1000]");
+      c->region_pct = (uint32_t)v;
       return 0;
     case L5DH_PARAM_MERGE_RCCL_1RANK:
       c->rccl_1rank = v != 0;
@@ -1355,11 +1408,7 @@ int l5dh_merge(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, in
   hipSetDevice(c->device);
   int r;
   if ((r = merge_export(c))) return r;
-  NCCLCHK(c, ncclGroupStart());
-  r = merge_collective(c, mode);
-  const ncclResult_t ge = ncclGroupEnd();
-  if (r) return r;
-  if (ge != ncclSuccess) return ncclfail(c, ge, "ncclGroupEnd");
+  if ((r = merge_collectives(&c, 1, mode))) return r;
   return merge_finish(c, mode, out, counts_out, totals_out, first, count);
 }
 
@@ -1375,14 +1424,7 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
     hipSetDevice(ctxs[i]->device);
     if ((r = merge_export(ctxs[i]))) return r;
   }
-  NCCLCHK(ctxs[0], ncclGroupStart());
-  for (int i = 0; i < n && !r; ++i) {
-    hipSetDevice(ctxs[i]->device);
-    r = merge_collective(ctxs[i], mode);
-  }
-  const ncclResult_t ge = ncclGroupEnd();
-  if (r) return r;
-  if (ge != ncclSuccess) return ncclfail(ctxs[0], ge, "ncclGroupEnd");
+  if ((r = merge_collectives(ctxs, n, mode))) return r;
   for (int i = 0; i < n; ++i) {
     hipSetDevice(ctxs[i]->device);
     if ((r = merge_finish(ctxs[i], mode, outs ? outs[i] : nullptr, counts_outs ? counts_outs[i] : nullptr,
@@ -1390,6 +1432,15 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
                           counts ? counts + i : nullptr)))
       return r;
   }
+  return 0;
+}
+
+int l5dh_merge_bytes(l5dh_ctx* c, uint64_t* dense, uint64_t* encoded, uint64_t* sent) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (dense) *dense = c->m_dense_bytes;
+  if (encoded) *encoded = c->m_encoded_bytes;
+  if (sent) *sent = c->m_sent_bytes;
   return 0;
 }
 

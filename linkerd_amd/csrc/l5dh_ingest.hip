@@ -1,488 +1,301 @@
-// l5dh_ingest.hip -- ingest-side kernels (Metric.Stat.add, batched).
+// l5dh_ingest.hip -- ingest-side kernels (Metric.Stat.add, batched): a two-level
+// partition of the COO batch into capacity-planned regions, with no counting pass.
 //
-//   k_count    LDS tile histogram of each slab of the COO batch -> table[g][t]
-//   k_colscan  per tile, exclusive prefix over slabs (in place) + tile totals
-//   k_tilescan exclusive prefix over tiles -> tile_base[F+1] (final layout)
-//   k_bin1     level 1: slab -> super-tiles (64 tiles) and direct tiles, LDS
-//              counting sort of 16K-sample sub-chunks, run writes
-//   k_bin2     level 2: (super-tile, slab block) -> per-(slab, tile) segments
-//   k_bin      single-level alternative (direct scatter)
+//   k_rsample  ids of 2^20 evenly spaced samples (every sample of a smaller batch)
+//              counted per (tile, half) key
+//   k_rplan1   this batch's direct tiles (the biggest estimated) and the level-1 bin
+//              regions (super-tiles; two half-bins per direct tile), sized from the
+//              previous batch's exact key counts and this batch's sample
+//   k_rbin1    level 1: LDS counting sort of 16K-sample sub-chunks by bin; each run's
+//              place in its bin's region comes from ONE returning global atomic per
+//              (sub-chunk, bin) on the bin's cursor (order inside a region is free:
+//              integer sums do not depend on it)
+//   k_rfix1    a run that did not fit its region -> exact regions from the cursors
+//              and a second k_rbin1 pass (launched always, it exits unless needed);
+//              the direct keys' ranges; the invalid-id count to the host
+//   k_rplan2   level-2 regions of the other keys; level-2 items (16K records of a
+//              super-tile's level-1 region)
+//   k_rbin2    level 2: an item LDS-sorted by key into 16-bit records (series in
+//              tile | bucket) in its keys' regions; value sums folded into sumfix
+//   k_rfix2    exact key counts -> kprev (the next batch's prediction); overflow ->
+//              exact regions and a second k_rbin2 pass
 //
-// Records (l5dh_kernels.hpp): [31:26] tile in super-tile | [25:21] series in
-//   tile | [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped: the
-//   exact sum difference went to sumfix[series], integer atomics, order free).
+// Level-1 record (rec32): [31:26] tile in super-tile | [25:21] series in tile |
+//   [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped: the exact sum
+//   contribution went to sumfix[series], integer atomics, order free).
 #include <algorithm>
 
 #include "l5dh_device.hpp"
-// L5DH_EXP (compile time, tools/mk_var.sh): timing-only variants, results invalid.
-//   4 k_count without hot-column aggregation, 8 k_count loads only,
-//   16 k_bin1 loads + ranking only (no scan, scatter or run writes),
-//   1024 k_bin1 run writes replaced by the same number of sequential stores,
-//   2048 ... by whole 64-B segments in 1024 interleaved sequential streams
-#ifndef L5DH_EXP
-#define L5DH_EXP 0
-#endif
-// hot count columns aggregated by ballot in k_count (2 or 4; the plan holds 4 hints)
-#ifndef L5DH_HK
-#define L5DH_HK 2
-#endif
-static_assert(L5DH_HK >= 2 && L5DH_HK <= 4, "k_count's tail path uses two hot columns; the plan holds four");
 
 namespace l5dh {
 namespace {
 
-constexpr int ST_TILES = 64;
-constexpr int ST_SHIFT = 11;  // 64 tiles x 32 series
-constexpr uint32_t NOKEY = 0xFFFFFFFFu;
-constexpr int NHOT = 8;       // k_bin1 bins counted in lane-private slots
-#ifndef L5DH_B2_ITEM
-#define L5DH_B2_ITEM 32768
-#endif
-constexpr uint32_t B2_ITEM = L5DH_B2_ITEM;  // target level-1 records per k_bin2 item
-static_assert(B2_ITEM >= 16384, "the plan's item map holds (2^30 / 16384 + 1024) items");
+constexpr uint32_t RSAMPLE = 1u << 20;  // sampled ids per batch
+constexpr int RS_WG = 64;               // k_rsample workgroups (<= 16384 draws each: u16 LDS counters)
+constexpr uint32_t INVALID = 0xFFFFFFFFu;
 
-// ------------------------------------------------------------------------
-// Count key of a valid sample: its tile, or for a split tile the column of its
-// half (F + 2 s + half).  sw[w] = {split bits of word w, split tiles before it}.
-__device__ __forceinline__ uint32_t count_key(uint32_t s, uint32_t F, uint2 sw) {
-  const uint32_t t = s >> TILE_SHIFT;
-  const uint32_t bit = 1u << (t & 31u);
-  const uint32_t sk = F + 2u * (sw.y + (uint32_t)__popc(sw.x & (bit - 1u))) + ((s >> 4) & 1u);
-  return (sw.x & bit) ? sk : t;
-}
+__device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
-__global__ __launch_bounds__(WG) void k_count(const uint32_t* __restrict__ series, size_t n, size_t per, uint32_t S,
-                                              uint32_t F, uint32_t* __restrict__ table, uint32_t* __restrict__ err,
-                                              const uint32_t* __restrict__ hint, const uint32_t* __restrict__ split,
-                                              int vec) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t C = F + COLS;
-  uint2* sw = reinterpret_cast<uint2*>(smem);  // [1024] split words
-  uint32_t* cnt = smem + 2048;                  // [C]
-  const uint32_t NW = (F + 31) / 32;
-  for (uint32_t t = threadIdx.x; t < C; t += WG) cnt[t] = 0;
-  for (uint32_t w = threadIdx.x; w < NW; w += WG) sw[w] = make_uint2(split[SPLIT_BITS + w], split[SPLIT_PRE + w]);
-  __syncthreads();
-  const size_t lo = (size_t)blockIdx.x * per;
-  const size_t hi = lo + per < n ? lo + per : n;
-  uint32_t hk[L5DH_HK];  // hot columns of the previous batch (aggregation only)
-#pragma unroll
-  for (int h = 0; h < L5DH_HK; ++h) hk[h] = hint[h] < C && !(L5DH_EXP & 4) ? hint[h] : 0xFFFFFFFFu;
-  bool bad = false;
-  if (lo < hi) {
-    size_t done = lo;
-    if (vec) {  // lo and the base pointer are 16-B aligned
-      const size_t nv = (hi - lo) >> 2;
-      const uint4* __restrict__ p = reinterpret_cast<const uint4*>(series + lo);
-      size_t i = threadIdx.x;
-      const size_t wlast = threadIdx.x | 63;  // last lane of this wave: uniform loop bound
-      // software-pipelined: the next two groups of 4 x 16 B per thread are in flight
-      // during this one's LDS counting, so the HBM stream does not pause behind it
-      auto full = [&](size_t j) { return wlast - threadIdx.x + j + 3 * WG < nv; };
-      auto load4 = [&](size_t j, uint4 (&x)[4]) {
-        if (full(j)) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = p[j + q * WG];
-        }
-      };
-      uint4 n0[4], n1[4];
-      load4(i, n0);
-      if (!(L5DH_EXP & 128)) load4(i + 4 * WG, n1);
-      for (; full(i); i += 4 * WG) {
-        const uint4 a = n0[0], b = n0[1], c = n0[2], d = n0[3];
-        if (!(L5DH_EXP & 128)) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) n0[q] = n1[q];
-          load4(i + 8 * WG, n1);
-        } else {
-          load4(i + 4 * WG, n0);
-        }
-        if (L5DH_EXP & 8) {  // timing: loads only
-          asm volatile("" ::"v"(a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w));
-          continue;
-        }
-        const uint32_t sv[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
-        uint2 wv[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) wv[k] = sw[(sv[k] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
-        uint32_t key[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const bool ok = sv[k] < S;
-          bad |= !ok;
-          key[k] = ok ? count_key(sv[k], F, wv[k]) : 0xFFFFFFFFu;
-        }
-        hot_inc_batch<L5DH_HK, 16>(cnt, key, hk);
-      }
-      for (; i - threadIdx.x < nv; i += WG) {  // convergent: out-of-range lanes pass invalid ids
-        uint4 a = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (i < nv) a = p[i];
-        const bool in = i < nv;
-        auto one_in = [&](uint32_t s) {
-          const bool ok = in && s < S;
-          bad |= in && !ok;
-          hot_inc(cnt, ok ? count_key(s, F, sw[s >> (TILE_SHIFT + 5)]) : 0u, ok, hk[0], hk[1]);
-        };
-        one_in(a.x); one_in(a.y); one_in(a.z); one_in(a.w);
-      }
-      done = lo + (nv << 2);
-    }
-    for (size_t i0 = done; i0 < hi; i0 += WG) {  // convergent tail (the aggregation needs whole waves)
-      const size_t i = i0 + threadIdx.x;
-      const uint32_t s = i < hi ? series[i] : 0xFFFFFFFFu;
-      const bool ok = s < S;
-      bad |= i < hi && !ok;
-      hot_inc(cnt, ok ? count_key(s, F, sw[s >> (TILE_SHIFT + 5)]) : 0u, ok, hk[0], hk[1]);
-    }
-  }
-  if (bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
-  __syncthreads();
-  uint32_t* row = table + (size_t)blockIdx.x * C;
-  for (uint32_t t = threadIdx.x; t < C; t += WG) row[t] = cnt[t];
-}
-
-// WG = 64 tiles x 16 slab groups.
-__global__ __launch_bounds__(1024) void k_colscan(uint32_t* __restrict__ table, int G, uint32_t C,
-                                                  uint32_t* __restrict__ tile_tot) {
-  __shared__ uint32_t part[16][64];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const uint32_t t = blockIdx.x * 64 + lane;
-  const int gper = (G + 15) / 16;
-  const int g0 = w * gper;
-  const int g1 = min(G, g0 + gper);
-  // G <= 512: a wave's <= 32 slabs are loaded at once (one memory latency, not one
-  // per slab: the in-place prefix stores would otherwise order every load)
-  constexpr int GW = 32;
-  uint32_t v[GW];
-  uint32_t s = 0;
-#pragma unroll
-  for (int k = 0; k < GW; ++k) {
-    v[k] = (t < C && g0 + k < g1) ? table[(size_t)(g0 + k) * C + t] : 0u;
-    s += v[k];
-  }
-  part[w][lane] = s;
-  __syncthreads();
-  if (w == 0) {
-    uint32_t acc = 0;
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t x = part[k][lane];
-      part[k][lane] = acc;
-      acc += x;
-    }
-    if (t < C) tile_tot[t] = acc;
-  }
-  __syncthreads();
-  if (t < C) {
-    uint32_t acc = part[w][lane];
-#pragma unroll
-    for (int k = 0; k < GW; ++k)
-      if (g0 + k < g1) {
-        table[(size_t)(g0 + k) * C + t] = acc;
-        acc += v[k];
-      }
-  }
-}
-__global__ __launch_bounds__(1024) void k_tilescan(uint32_t* __restrict__ coltot, uint32_t F,
-                                                   const uint32_t* __restrict__ split, uint32_t* __restrict__ tile_base) {
-  __shared__ uint32_t lds[17];
-  const uint32_t per = (F + 1023) / 1024;
-  const uint32_t t0 = threadIdx.x * per;
-  // a thread's tiles: totals of split tiles are the sums of their halves
-  auto tile_total = [&](uint32_t t, uint32_t v) {
-    const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
-    const uint32_t bit = 1u << (t & 31u);
-    if (wd & bit) {
-      const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
-      v += coltot[F + 2 * si] + coltot[F + 2 * si + 1];
-      coltot[t] = v;
-    }
-    return v;
-  };
-  constexpr int PT = 32;  // F <= 32 K tiles: all of a thread's loads issued at once
-  uint32_t v[PT];
-  uint32_t s = 0, tot;
-  if (per <= PT) {
-    // a thread's <= 32 consecutive tiles span <= 2 split words; every load (totals,
-    // split words, half totals) is issued before any store (the split tiles' sums
-    // are written back to coltot[t] after the loads)
-    const uint32_t wb = t0 >> 5;
-    const uint32_t sw0 = t0 < F ? split[SPLIT_BITS + wb] : 0u, sp0 = t0 < F ? split[SPLIT_PRE + wb] : 0u;
-    const uint32_t sw1 = (wb + 1) * 32 < F ? split[SPLIT_BITS + wb + 1] : 0u;
-    const uint32_t sp1 = (wb + 1) * 32 < F ? split[SPLIT_PRE + wb + 1] : 0u;
-    uint32_t h[PT];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t t = t0 + k;
-      const bool in = (uint32_t)k < per && t < F;
-      v[k] = in ? coltot[t] : 0u;
-      const bool hi = (t >> 5) != wb;
-      const uint32_t wd = hi ? sw1 : sw0, bit = 1u << (t & 31u);
-      h[k] = 0u;
-      if (in && (wd & bit)) {
-        const uint32_t si = (hi ? sp1 : sp0) + (uint32_t)__popc(wd & (bit - 1u));
-        h[k] = 1u + coltot[F + 2 * si] + coltot[F + 2 * si + 1];  // +1: split (a split tile may be empty)
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      if (h[k]) {
-        v[k] += h[k] - 1u;
-        coltot[t0 + k] = v[k];
-      }
-      s += v[k];
-    }
-    uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
-#pragma unroll
-    for (int k = 0; k < PT; ++k)
-      if ((uint32_t)k < per && t0 + k < F) {
-        tile_base[t0 + k] = acc;
-        acc += v[k];
-      }
+// Region capacity of a bin or key: the larger of the previous batch's exact records
+// (+1/16 + 4 sigma) and this batch's sample estimate (+4 sigma), plus a pad; exact
+// when the sample was the whole batch.  A region that still overflows is redone
+// with exact sizes (k_rfix1 / k_rfix2), so this only has to be right almost always.
+// `pct` scales the result (L5DH_PARAM_REGION_PCT; below 100 forces the redo path).
+__device__ __forceinline__ uint32_t rcap(double prev, double e, double s, bool exact, double pad, uint32_t align,
+                                         uint32_t pct) {
+  double c;
+  if (exact) {
+    c = e;
   } else {
-    for (uint32_t k = 0; k < per && t0 + k < F; ++k) s += tile_total(t0 + k, coltot[t0 + k]);
-    uint32_t acc = block_excl_scan<1024>(s, lds, &tot);
-    for (uint32_t k = 0; k < per && t0 + k < F; ++k) {
-      tile_base[t0 + k] = acc;
-      acc += coltot[t0 + k];
-    }
+    const double a = prev > 0.0 ? prev * 1.0625 + 4.0 * sqrt(prev) : 0.0;
+    const double b = (e + 4.0 * sqrt(e + 1.0)) * s;
+    c = ceil(fmax(a, b)) + pad;
   }
-  if (threadIdx.x == 0) tile_base[F] = tot;
-}
-// k_tilescan + k_seginfo in one workgroup, through LDS: the column totals are loaded
-// coalesced (a thread's 32 consecutive tiles read strided from global memory were
-// ~30 us on C3), split tiles add their halves, every thread scans its 32 consecutive
-// tiles from LDS (one pad word per 32: no bank conflicts), and tile_base goes out
-// coalesced.  F <= 32768.
-constexpr uint32_t tpad(uint32_t t) { return t + (t >> 5); }
-__global__ __launch_bounds__(1024) void k_tilescan_seg(uint32_t* __restrict__ coltot, uint32_t F,
-                                                       const uint32_t* __restrict__ split,
-                                                       uint32_t* __restrict__ tile_base, uint32_t* __restrict__ sinfo) {
-  extern __shared__ uint32_t tl[];  // [tpad(F) + 1]
-  __shared__ uint32_t lds[17];
-  const uint32_t NS = split[0];
-  uint16_t* map = reinterpret_cast<uint16_t*>(sinfo + SINFO_MAP);
-  for (uint32_t t = threadIdx.x; t < F; t += 1024) {
-    tl[tpad(t)] = coltot[t];
-    map[t] = NO_SPLIT;
-  }
-  __syncthreads();
-  // split tiles: their samples were counted in the two half columns
-  for (uint32_t si = threadIdx.x; si < NS; si += 1024) {
-    const uint32_t t = split[SPLIT_LIST + si];
-    const uint32_t h0 = coltot[F + 2 * si], h1 = coltot[F + 2 * si + 1];
-    const uint32_t v = tl[tpad(t)] + h0 + h1;
-    tl[tpad(t)] = v;
-    coltot[t] = v;  // read as the tile's total by k_stplan
-    sinfo[1 + si] = t;
-    sinfo[SINFO_H0 + si] = h0;
-    map[t] = (uint16_t)si;
-  }
-  if (threadIdx.x == 0) sinfo[0] = NS;
-  __syncthreads();
-  constexpr int PT = 32;
-  const uint32_t t0 = threadIdx.x * PT;
-  uint32_t v[PT], sum = 0, tot;
-#pragma unroll
-  for (int k = 0; k < PT; ++k) {
-    v[k] = t0 + k < F ? tl[tpad(t0 + k)] : 0u;
-    sum += v[k];
-  }
-  uint32_t acc = block_excl_scan<1024>(sum, lds, &tot);
-#pragma unroll
-  for (int k = 0; k < PT; ++k)
-    if (t0 + k < F) {
-      tl[tpad(t0 + k)] = acc;
-      acc += v[k];
-    }
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < F; t += 1024) tile_base[t] = tl[tpad(t)];
-  if (threadIdx.x == 0) tile_base[F] = tot;
+  if (pct != 100) c = floor(c * (double)pct / 100.0);
+  return round_up((uint32_t)fmin(c, 1073741824.0), align);
 }
 
-__global__ __launch_bounds__(1024) void k_seginfo(const uint32_t* __restrict__ split, const uint32_t* __restrict__ coltot,
-                                                  uint32_t F, uint32_t* __restrict__ sinfo) {
-  const uint32_t NS = split[0];
-  uint16_t* map = reinterpret_cast<uint16_t*>(sinfo + SINFO_MAP);
-  for (uint32_t t = threadIdx.x; t < F; t += 1024) map[t] = NO_SPLIT;
+// Exclusive block scan of u64 values (one per thread), NT = 1024.
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* lds /*[17]*/, uint64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_scan(v);
+  if (lane == 63) lds[w] = incl;
   __syncthreads();
-  if (threadIdx.x == 0) sinfo[0] = NS;
-  for (uint32_t si = threadIdx.x; si < NS; si += 1024) {
-    const uint32_t t = split[SPLIT_LIST + si];
-    sinfo[1 + si] = t;
-    sinfo[SINFO_H0 + si] = coltot[F + 2 * si];
-    map[t] = (uint16_t)si;
-  }
-}
-
-// One-tile series spaces (S <= 32: C1, the head shard of a many-way C3): the
-// tile's records are the samples in input order -- no counting pass, no partition.
-// An invalid id becomes 0xFFFFFFFF, which no valid record equals (its bucket field
-// would be 2047) and the accumulate kernels skip; the tile's range is the batch.
-__global__ __launch_bounds__(256) void k_encode1(const uint32_t* __restrict__ series, const float* __restrict__ values,
-                                                 size_t n, uint32_t S, Tables tb, uint32_t* __restrict__ records,
-                                                 int64_t* __restrict__ sumfix, uint32_t* __restrict__ tile_base,
-                                                 uint32_t* __restrict__ err, int vec) {
-  bool bad = false;
-  auto enc = [&](uint32_t s, float f) -> uint32_t {
-    if (s >= S) {
-      bad = true;
-      return 0xFFFFFFFFu;
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t q = lds[k];
+      lds[k] = acc;
+      acc += q;
     }
-    return ((s & (TILE - 1)) << 21) | payload1(s, f, tb, sumfix);
-  };
-  const size_t tid = (size_t)blockIdx.x * 256 + threadIdx.x, nth = (size_t)gridDim.x * 256;
-  size_t done = 0;
-  if (vec) {  // 16-B loads and stores
-    const size_t nv = n >> 2;
-    for (size_t i = tid; i < nv; i += nth) {
-      const uint4 a = reinterpret_cast<const uint4*>(series)[i];
-      const float4 v = reinterpret_cast<const float4*>(values)[i];
-      reinterpret_cast<uint4*>(records)[i] = make_uint4(enc(a.x, v.x), enc(a.y, v.y), enc(a.z, v.z), enc(a.w, v.w));
-    }
-    done = nv << 2;
+    lds[16] = acc;
   }
-  for (size_t i = done + tid; i < n; i += nth) records[i] = enc(series[i], values[i]);
-  if (bad) atomicAdd(err, 1u);  // monotonic, like k_count's
-  if (tid == 0) {
-    tile_base[0] = 0u;
-    tile_base[1] = (uint32_t)n;
-  }
-}
-
-// Single-level: scatter records to the slab's exclusive (slab, tile) segment.
-__global__ __launch_bounds__(WG) void k_bin(const uint32_t* __restrict__ series, const float* __restrict__ values,
-                                            size_t n, size_t per, uint32_t S, uint32_t F,
-                                            const uint32_t* __restrict__ table, const uint32_t* __restrict__ tile_base,
-                                            Tables tb, uint32_t* __restrict__ records, int64_t* __restrict__ sumfix,
-                                            int vec) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* cur = smem;
-  const uint32_t* row = table + (size_t)blockIdx.x * (F + COLS);  // counted without split tiles
-  for (uint32_t t = threadIdx.x; t < F; t += WG) cur[t] = tile_base[t] + row[t];
   __syncthreads();
-  const size_t lo = (size_t)blockIdx.x * per;
-  const size_t hi = lo + per < n ? lo + per : n;
-  if (lo >= hi) return;
-  auto one = [&](uint32_t s, float f) {
-    if (s >= S) return;
-    const uint32_t rec = (((s >> TILE_SHIFT) & 63u) << 26) | ((s & (TILE - 1)) << 21) | payload1(s, f, tb, sumfix);
-    records[atomicAdd(&cur[s >> TILE_SHIFT], 1u)] = rec;
-  };
-  size_t done = lo;
-  if (vec) {
-    const size_t nv = (hi - lo) >> 2;
-    const uint4* ps = reinterpret_cast<const uint4*>(series + lo);
-    const float4* pv = reinterpret_cast<const float4*>(values + lo);
-    for (size_t i = threadIdx.x; i < nv; i += WG) {
-      const uint4 s = ps[i];
-      const float4 f = pv[i];
-      one(s.x, f.x); one(s.y, f.y); one(s.z, f.z); one(s.w, f.w);
-    }
-    done = lo + (nv << 2);
-  }
-  for (size_t i = done + threadIdx.x; i < hi; i += WG) one(series[i], values[i]);
+  const uint64_t r = lds[w] + incl - v;
+  *total = lds[16];
+  __syncthreads();
+  return r;
 }
 
 // ------------------------------------------------------------------------
-// Level 1.  LDS: stage[CH1] u32, stage_st[CH1] u16, stcnt/stoff/stcur[FS_MAX].
+// Sample: key = series >> 4 = 2 tile + half.  LDS: u16 pairs of keys.
+__global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ series, size_t n, uint32_t S, uint32_t K,
+                                                  uint32_t* __restrict__ kest) {
+  extern __shared__ uint32_t c[];  // [(K + 1) / 2]
+  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) c[i] = 0;
+  __syncthreads();
+  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
+  const uint64_t per = (m + RS_WG - 1) / RS_WG;
+  const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
+  for (uint64_t k = k0 + threadIdx.x; k < k1; k += 1024) {
+    const uint64_t i = m == n ? k : k * n / m;  // evenly spaced draws
+    const uint32_t s = series[i];
+    if (s < S) {
+      const uint32_t key = s >> 4;
+      atomicAdd(&c[key >> 1], (key & 1u) ? 0x10000u : 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) {
+    const uint32_t x = c[i];
+    if (x & 0xFFFFu) atomicAdd(&kest[2 * i], x & 0xFFFFu);
+    if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
+  }
+}
 
-// Level 1.  Bins = the FS super-tiles (records of their non-direct tiles, into
-// scratch1) and two bins per direct tile (records straight into the final layout;
-// a split tile's half 0 from the tile's start, half 1 after all half-0 records; an
-// unsplit tile's bins share one range, the even bin's run first), plus a trash bin for sample slots with no sample (batch
-// tail, ids >= S: counted as errors by k_count) written to scratch1[n ..).  Both
-// arrays share the final layout's index space: slab g's records of direct tile t
-// start at tile_base[t] + pre[g][t]; its level-1 records of super-tile j at
-// tile_base[j*64] + sum of pre[g][t] over the non-direct t of j.
-// Per CH1-slot sub-chunk (every slot lands in exactly one bin, so the body has
-// no per-sample branches): one LDS atomic ranks each slot in its bin (the NHOT
-// hottest bins count in lane-private slots: no same-address serialization), a
-// scan gives bin offsets, each slot is staged at its sorted position WITH its
-// destination ({record, dst | direct << 31}), and all CH1 stage entries are
-// written in order.  Batches are < 2^30 samples.
-// LDS: stage[CH1] uint2, cnt[BINS], oc[BINS] {off, cur | direct << 31}, direct
-// words {bits, prefix}, hot slots, lane-private hot counters (+1 zero row).
-template <int CH1, int NT, int WPS, bool HS_ALWAYS>
-__global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
-                                                size_t n, size_t per, uint32_t S, uint32_t F,
-                                                const uint32_t* __restrict__ pre,
-                                                const uint32_t* __restrict__ tile_base, Tables tb,
-                                                const uint32_t* __restrict__ plan, const uint32_t* __restrict__ coltot,
-                                                const uint32_t* __restrict__ split, uint32_t* __restrict__ out1, uint32_t* __restrict__ records,
-                                                int64_t* __restrict__ sumfix, int vec, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint2* stage = reinterpret_cast<uint2*>(smem);                   // [CH1]
-  uint32_t* cnt = smem + 2 * CH1;                                  // [BIN1_BINS]
-  uint2* oc = reinterpret_cast<uint2*>(cnt + BIN1_BINS);           // [BIN1_BINS] {stage offset, cursor | direct << 31}
-  uint2* dw = oc + BIN1_BINS;                                      // [1024] {direct bits, direct tiles before}
-  uint8_t* hslot = reinterpret_cast<uint8_t*>(dw + 1024);          // [BIN1_BINS] hot slot of a bin (NHOT: none)
-  uint32_t* hcnt = reinterpret_cast<uint32_t*>(hslot + BIN1_BINS); // [NHOT + 1][64] lane-private hot counters
-  uint32_t* dun = hcnt + (NHOT + 1) * 64;                          // [8] unsplit direct tiles (bit d)
+// ------------------------------------------------------------------------
+// Level-1 plan, one workgroup.  Thread j owns tiles [32 j, 32 j + 32) (F <= 32768)
+// and bin j.  Direct tiles: the <= dmax tiles with the most estimated records, at
+// least max(thr_min, 2^k), k the smallest power keeping <= dmax of them.
+__global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
+                                                 const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
+                                                 size_t cap32, uint32_t thr_min, uint32_t dmax, uint32_t pct) {
+  __shared__ uint32_t lh[33];
+  __shared__ uint32_t sthr;
+  __shared__ uint4 lds4[17];
+  __shared__ uint64_t l64[17];
+  __shared__ uint32_t dl[DIRECT_MAX + 1];
+  __shared__ uint32_t capl[BIN1_BINS];
+  __shared__ double predl[BIN1_BINS];
+  __shared__ unsigned long long best[16];
+  const MetaLayout L = meta_layout(F);
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t NW = (F + 31) / 32;
-  const uint32_t ND = plan[PLAN_ND];
-  // lane-private counters for the hottest bins (development variant, HS_ALWAYS)
-  const bool HS = HS_ALWAYS;
-  // When one bin holds >= half the batch (a single-series or few-series shard: every
-  // lane of a wave would otherwise serialize on its LDS counter), the batch's two
-  // hottest bins are ranked by wave ballots; measured (tools/ab_var.py, same context):
-  // 41 % faster on C3's first 8-way shard, 2 % slower on C3 (hottest bin 23 %), 17 %
-  // slower on C2 (no hot bin) -- so only past that share.  Variant bit 0: never.
-  const bool hotrank = !HS && plan[PLAN_HS] != 0u && !((dbg >> 27) & 1);
-  const uint32_t hb0 = plan[3 * FS + 1], hb1 = plan[3 * FS + 2];  // NOKEY: none
+  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
+  const bool exact = m == n;
+  const double s = m ? (double)n / (double)m : 1.0;
+  const uint32_t j = threadIdx.x, t0 = j * 32;
+  if (j < 33) lh[j] = 0;
+  capl[j] = 0;
+  predl[j] = 0.0;
+  __syncthreads();
+  auto tile_est = [&](int k) -> uint32_t {  // sampled ids of this thread's tile t0 + k
+    const uint32_t t = t0 + k;
+    return t < F ? kest[2 * t] + kest[2 * t + 1] : 0u;
+  };
+  uint32_t dbits = 0;
+  for (int k = 0; k < 32; ++k) {
+    const double est = (double)tile_est(k) * s;
+    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
+    if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
+  }
+  __syncthreads();
+  if (j == 0) {
+    uint32_t cum = 0, thr = 0xFFFFFFFFu;
+    int kbest = 32;
+    if (dmax > 0)
+      for (int k = 31; k >= 0; --k) {
+        cum += lh[k];
+        if (cum > dmax) break;
+        kbest = k;
+      }
+    if (kbest < 32) thr = max(max(thr_min, 1u), 1u << kbest);
+    sthr = thr;
+  }
+  __syncthreads();
+  const uint32_t thr = sthr;
+  for (int k = 0; k < 32; ++k) {
+    const double est = (double)tile_est(k) * s;
+    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
+    if (t0 + k < F && e >= thr) dbits |= 1u << k;
+  }
+  uint32_t cv[4] = {(uint32_t)__popc(dbits), 0u, 0u, 0u}, ct[4];
+  block_excl_scan4<1024>(cv, lds4, ct);
+  const uint32_t ND = ct[0];
+  if (j < 1024) {
+    meta[L.dbits() + j] = j < NW ? dbits : 0u;
+    meta[L.dpre() + j] = cv[0];
+  }
+  {
+    uint32_t x = dbits, di = cv[0];
+    while (x) {
+      const uint32_t k = (uint32_t)(__ffs((int)x) - 1);
+      x &= x - 1u;
+      dl[di] = t0 + k;
+      meta[L.dlist() + di] = t0 + k;
+      ++di;
+    }
+  }
+  // super-tile bins: this thread's non-direct tiles, summed with its partner (the other
+  // half of the super-tile is lane j ^ 1 of the same wave)
+  double P = 0.0, E = 0.0;
+  for (int k = 0; k < 32; ++k) {
+    const uint32_t t = t0 + k;
+    if (t < F && !((dbits >> k) & 1u)) {
+      P += (double)kprev[2 * t] + (double)kprev[2 * t + 1];
+      E += (double)tile_est(k);
+    }
+  }
+  P += __shfl_xor(P, 1, 64);
+  E += __shfl_xor(E, 1, 64);
+  if ((j & 1u) == 0 && (j >> 1) < FS) {
+    const uint32_t b = j >> 1;
+    capl[b] = rcap(P, E, s, exact, 256.0, 4, pct);
+    predl[b] = fmax(P, E * s);
+  }
+  __syncthreads();  // dl complete
+  const uint32_t TB = FS + 2 * ND;
+  if (j >= FS && j < TB) {  // direct half-bins
+    const uint32_t t = dl[(j - FS) >> 1], h = (j - FS) & 1u;
+    const double p = (double)kprev[2 * t + h], e = (double)kest[2 * t + h];
+    capl[j] = rcap(p, e, s, exact, 256.0, 4, pct);
+    predl[j] = fmax(p, e * s);
+  }
+  __syncthreads();
+  uint64_t total;
+  uint64_t base = block_excl_scan64((uint64_t)capl[j], l64, &total);
+  if (total + 16 > cap32) {  // too big for the buffer: scale down (an overflow is redone exactly)
+    const double f = (double)(cap32 - 16) / (double)total;
+    const uint32_t c2 = (uint32_t)((double)capl[j] * f) & ~3u;
+    base = block_excl_scan64((uint64_t)c2, l64, &total);
+    capl[j] = c2;
+  }
+  meta[L.bbase() + j] = (uint32_t)base;
+  meta[L.bcap() + j] = j < TB ? capl[j] : 0u;
+  meta[L.bcnt() + j] = 0u;
+  // the two biggest bins by prediction, for the ballot ranking of k_rbin1
+  const int lane = j & 63, w = j >> 6;
+  auto block_max = [&](unsigned long long v) -> unsigned long long {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const unsigned long long o = __shfl_xor(v, d, 64);
+      v = o > v ? o : v;
+    }
+    __syncthreads();
+    if (lane == 0) best[w] = v;
+    __syncthreads();
+    unsigned long long r = 0;
+    for (int q = 0; q < 16; ++q) r = best[q] > r ? best[q] : r;
+    return r;
+  };
+  const unsigned long long mine = j < TB ? (((unsigned long long)fmin(predl[j], 4.0e12) << 10) | j) : 0ull;
+  const unsigned long long b1 = block_max(mine);
+  const unsigned long long b2 = block_max(mine == b1 ? 0ull : mine);
+  double psum = j < TB ? predl[j] : 0.0;
+  psum = (double)wave_sum((uint64_t)psum);
+  __syncthreads();
+  if (lane == 0) best[w] = (unsigned long long)psum;
+  __syncthreads();
+  if (j == 0) {
+    unsigned long long all = 0;
+    for (int q = 0; q < 16; ++q) all += best[q];
+    uint32_t* hdr = meta + L.hdr();
+    hdr[H_ND] = ND;
+    hdr[H_OV1] = 0;
+    hdr[H_REDO1] = 0;
+    hdr[H_OV2] = 0;
+    hdr[H_REDO2] = 0;
+    hdr[H_HB0] = (b1 >> 10) ? (uint32_t)(b1 & 1023u) : NOKEY;
+    hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
+    hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
+    hdr[H_EXACT] = exact ? 1u : 0u;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Level 1.  Bins: the FS super-tiles (their non-direct records, for level 2), two
+// half-bins per direct tile (final records), and a trash bin (slots with no valid
+// sample: the batch's ragged end, ids >= S) that is never written.  Per CH1-slot
+// sub-chunk: one LDS atomic ranks each slot in its bin (or a wave ballot, for the
+// two hottest bins when one holds >= half the batch), every wave reserves the runs
+// of 64 bins with one returning global atomic per non-empty bin, a one-wave scan
+// gives stage offsets, each slot is staged sorted with its bin, and the stage is
+// written in order to run base + position.  pass 1 (the redo) exits unless k_rfix1
+// asked for it and adds nothing to sumfix or the error counter.
+// LDS: stage[CH1] uint2, cnt[BINS], ocx[BINS] {stage offset, run base}, direct words.
+constexpr size_t rbin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + 16; }
+
+template <int CH1, int NT>
+__global__ __launch_bounds__(NT, 1) void k_rbin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                                 size_t n, size_t per, uint32_t S, uint32_t F, Tables tb,
+                                                 uint32_t* __restrict__ meta, uint32_t* __restrict__ rec32,
+                                                 int64_t* __restrict__ sumfix, uint32_t* __restrict__ err, int vec,
+                                                 int pass) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint2* stage = reinterpret_cast<uint2*>(smem);          // [CH1] {record, bin}
+  uint32_t* cnt = smem + 2 * CH1;                         // [BIN1_BINS]
+  uint2* ocx = reinterpret_cast<uint2*>(cnt + BIN1_BINS); // [BIN1_BINS] {stage offset, run base | INVALID}
+  uint2* dw = ocx + BIN1_BINS;                            // [1024] {direct bits, direct tiles before}
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
+  uint32_t* bcnt = meta + L.bcnt();
+  const uint32_t* bbase = meta + L.bbase();
+  const uint32_t* bcap = meta + L.bcap();
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t NW = (F + 31) / 32;
+  const uint32_t ND = hdr[H_ND];
+  const uint32_t TB = FS + 2 * ND;
+  const bool hotrank = hdr[H_HS] != 0u;
+  const uint32_t hb0 = hdr[H_HB0], hb1 = hdr[H_HB1];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const uint32_t TB = FS + 2 * ND;  // trash bin (TB + 1 <= BIN1_BINS bins)
-  const uint32_t trash = (uint32_t)n;  // scratch1 has n + CH1 + 16 entries
-  const uint32_t* prow = pre + (size_t)blockIdx.x * (F + COLS);
-  for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(plan[PLAN_DBITS + w], plan[PLAN_DPRE + w]);
-  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) {
-    uint32_t sl = NHOT;
-#pragma unroll
-    for (int q = 0; q < NHOT; ++q)
-      if (plan[3 * FS + 1 + q] == b) sl = (uint32_t)q;
-    hslot[b] = (uint8_t)sl;
-    cnt[b] = 0;
-  }
-  for (uint32_t i = threadIdx.x; i < (NHOT + 1) * 64; i += NT) hcnt[i] = 0;
-  // super-tile cursors: level-1 records of this slab before super-tile j; one
-  // wave per super-tile, a lane per tile (independent, coalesced loads)
-  for (uint32_t t = threadIdx.x; t < FS * ST_TILES; t += NT) {
-    uint32_t v = 0;
-    if (t < F && !((plan[PLAN_DBITS + (t >> 5)] >> (t & 31u)) & 1u)) {  // direct tiles have no level-1 records
-      const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
-      const uint32_t bit = 1u << (t & 31u);
-      if (wd & bit) {  // split: its count is in the two half columns
-        const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
-        v = prow[F + 2 * si] + prow[F + 2 * si + 1];
-      } else {
-        v = prow[t];
-      }
-    }
-    v = wave_sum(v);
-    if (lane == 0) oc[t >> 6] = make_uint2(0u, tile_base[t] + v);
-  }
-  if (threadIdx.x < 8) dun[threadIdx.x] = 0u;
-  __syncthreads();
-  for (uint32_t h = threadIdx.x; h < 2 * ND; h += NT) {  // direct tile h/2: half 0 from its start, half 1 after it
-    const uint32_t si = plan[PLAN_DSI + (h >> 1)];
-    const uint32_t t = plan[PLAN_DLIST + (h >> 1)];
-    uint32_t at;
-    if (si == NOKEY) {
-      // unsplit direct tile (counted per tile): both bins share the slab's one range,
-      // the odd bin's cursor is canonical (the bin scan places the even bin's run first)
-      at = tile_base[t] + prow[t];
-      if (h & 1u) atomicOr(&dun[h >> 6], 1u << ((h >> 1) & 31u));
-    } else {
-      at = tile_base[t] + ((h & 1u) ? coltot[F + 2 * si] : 0u) + prow[F + 2 * si + (h & 1u)];
-    }
-    oc[FS + h] = make_uint2(0u, at | 0x80000000u);
-  }
-  if (threadIdx.x == 0) oc[TB] = make_uint2(0u, trash);
+  for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(meta[L.dbits() + w], meta[L.dpre() + w]);
+  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) cnt[b] = 0;
   __syncthreads();
   const size_t lo = (size_t)blockIdx.x * per;
   const size_t hi = lo + per < n ? lo + per : n;
+  bool bad = false;
   constexpr int PT = CH1 / NT;  // slots per thread: PT/4 groups of 4 consecutive
   for (size_t c0 = lo; c0 < hi; c0 += CH1) {
     uint32_t sv[PT];
@@ -503,21 +316,14 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         const bool in = i < hi;
         sv[k] = in ? series[i] : 0xFFFFFFFFu;
         fv[k] = in ? values[i] : 0.0f;
+        bad |= in && sv[k] >= S;
       }
     }
-    if (dbg & 8) {  // timing: loads only
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = 0; k < PT; ++k) x ^= sv[k] ^ __float_as_uint(fv[k]);
-      if (x == 0x12345678u) out1[threadIdx.x] = x;
-      continue;
-    }
-    // Per group of 4 slots: payloads (samples outside [0, V_ESC) take a rare
-    // path through this thread's still free stage slots), batched LDS reads of the
-    // direct words, branch-free bin selection, then one rank atomic per slot; hot
-    // bins count in lane-private counters.
+    // Per group of 4 slots: payloads (samples outside [0, V_ESC) take a rare path
+    // through this thread's still free stage slots), direct words, branch-free bins,
+    // one rank atomic per slot.
     uint32_t rec[PT];
-    uint32_t pk[PT];  // [13:0] local rank | [24:14] bin | [28:25] hot slot (NHOT: none)
+    uint32_t pk[PT];  // [13:0] rank | [24:14] bin
 #pragma unroll
     for (int g = 0; g < PT; g += 4) {
       uint32_t pl[4];
@@ -530,6 +336,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         const bool fast = __float_as_uint(f) < 0x49FFC000u;  // bits of (float)V_ESC
         pl[q] = fast ? (uint32_t)f : 0u;
         escm |= (!fast && sv[g + q] < S) ? (1u << q) : 0u;
+        if (vec && c0 + CH1 <= hi) bad |= sv[g + q] >= S;
       }
       if (__ballot(escm != 0u)) {
         uint32_t* tmp = reinterpret_cast<uint32_t*>(stage) + threadIdx.x * 8;
@@ -540,7 +347,9 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         }
 #pragma unroll 1
         for (int q = 0; q < 4; ++q)
-          if ((escm >> q) & 1u) tmp[2 * q] = payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix);
+          if ((escm >> q) & 1u)
+            tmp[2 * q] = pass == 0 ? payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix)
+                                   : payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, nullptr);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if ((escm >> q) & 1u) pl[q] = tmp[2 * q];
@@ -548,7 +357,7 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       uint2 dv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
-      uint32_t bn[4], sl[4];
+      uint32_t bn[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t s = sv[g + q];
@@ -559,32 +368,18 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
             FS + 2u * (dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw))) + ((s >> 4) & 1u);
         bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
       }
-      if (HS) {
+      if (!hotrank) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sl[q] = hslot[bn[q]];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool hot = sl[q] < (uint32_t)NHOT;
-          uint32_t* ctr = hot ? hcnt + sl[q] * 64u + (uint32_t)lane : cnt + bn[q];
-          pk[g + q] = atomicAdd(ctr, 1u) | (bn[q] << 14) | (sl[q] << 25);
-        }
+        for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
       } else {
-        if (!hotrank) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
-        }
+        for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
       }
       asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
     }
     if (hotrank) {
-      // ranks: the batch's two hottest bins (k_stplan; e.g. a Zipf head's direct tile,
-      // ~1/4 of C3) by wave ballots -- one LDS atomic per wave and bin for all PT
-      // slots, and consecutive stage slots for a wave's hot samples -- the other bins
-      // by one LDS atomic per slot.  Same-address atomics on a hot counter otherwise
-      // serialize (SQ_LDS_ADDR_CONFLICT) and their scattered stage slots conflict.
+      // the batch's two hottest bins by wave ballots: one LDS atomic per wave and bin,
+      // consecutive stage slots; the other bins by one LDS atomic per slot
       uint32_t wc0 = 0, wc1 = 0;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
@@ -609,31 +404,19 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
         r1 += (uint32_t)__popcll(x1);
       }
     }
-    if (L5DH_EXP & 16) {  // timing: loads + ranking only (no scan, scatter or run writes)
-      uint32_t x = 0;
-#pragma unroll
-      for (int k = 0; k < PT; ++k) x ^= pk[k] ^ rec[k];
-      if (x == 0x12345678u) out1[threadIdx.x] = x;
-      __syncthreads();
-      for (uint32_t j = threadIdx.x; j <= TB; j += NT) cnt[j] = 0;
-      __syncthreads();
-      continue;
-    }
     __syncthreads();
-    if (wv == 0) {  // one wave: hot-slot lane prefixes and totals, then the bin scan (DPP, no barriers)
-      if (HS) {
-        uint32_t hv[NHOT];
-#pragma unroll
-        for (int h = 0; h < NHOT; ++h) hv[h] = hcnt[h * 64 + lane];  // rows of unused slots are zero
-#pragma unroll
-        for (int h = 0; h < NHOT; ++h) {
-          const uint32_t x = wave_incl_scan32(hv[h]);
-          hcnt[h * 64 + lane] = x - hv[h];
-          const uint32_t hk = plan[3 * FS + 1 + h];
-          if (lane == 63 && hk != NOKEY) cnt[hk] = x;
-        }
-      }
-      uint32_t c[16];  // lane l scans bins [16 l, 16 l + 16)
+    // run reservations: wave w, lane l -> bin 64 w + l (one returning atomic per
+    // non-empty bin; the results are used only after the scan and the scatter)
+    const uint32_t rb_bin = (uint32_t)wv * 64u + (uint32_t)lane;
+    const uint32_t rc = rb_bin < TB ? cnt[rb_bin] : 0u;
+    uint32_t rold = 0, rbase = 0, rcapv = 0;
+    if (rc) {
+      rold = atomicAdd(&bcnt[rb_bin], rc);
+      rbase = bbase[rb_bin];
+      rcapv = bcap[rb_bin];
+    }
+    if (wv == 0) {  // one wave: the stage offsets (DPP scan of 16 bins per lane)
+      uint32_t c[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 v = *reinterpret_cast<const uint4*>(cnt + 16 * lane + 4 * q);
@@ -645,468 +428,318 @@ __global__ __launch_bounds__(NT, WPS) void k_bin1(const uint32_t* __restrict__ s
       uint32_t e = wave_incl_scan32(tl) - tl;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        oc[16 * lane + q].x = e;
+        ocx[16 * lane + q].x = e;
         e += c[q];
       }
-      // unsplit direct tiles: this sub-chunk's run of the even bin, then the odd bin's,
-      // from the shared cursor (held by the odd bin: the advance below adds both counts)
-      for (uint32_t d = (uint32_t)lane; d < ND; d += 64)
-        if ((dun[d >> 5] >> (d & 31u)) & 1u) {
-          const uint32_t b0 = FS + 2 * d;
-          const uint32_t base = oc[b0 + 1].y;
-          oc[b0].y = base;
-          oc[b0 + 1].y = base + cnt[b0];
-        }
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = (pk[k] >> 14) & 2047u;
-      const uint32_t r = (pk[k] & 16383u) + (HS ? hcnt[(pk[k] >> 25) * 64 + lane] : 0u);  // row NHOT is zero
-      const uint2 x = oc[bin];
-      stage[x.x + r] = make_uint2(rec[k], x.y + r);
+      stage[ocx[bin].x + (pk[k] & 16383u)] = make_uint2(rec[k], bin);
     }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < TB; j += NT) {  // cursors advance; the stage carries the destinations
-      oc[j].y += cnt[j];
-      cnt[j] = 0;
-    }
-    if (threadIdx.x == 0) cnt[TB] = 0;
-    if (HS)
-      for (uint32_t i = threadIdx.x; i < NHOT * 64; i += NT) hcnt[i] = 0;
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (trash entries land past scratch1[n])
-      const uint2 e = stage[(uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane];  // each wave: a contiguous PT x 64 range
-      if (L5DH_EXP & 1024)  // timing: the same stores, sequential (where the slots were read)
-        out1[c0 + threadIdx.x + k * NT] = e.x;
-      else if (L5DH_EXP & 2048) {  // timing: whole 64-B segments, 1024 interleaved sequential streams
-        const size_t idx = c0 + threadIdx.x + k * NT;
-        const size_t seg = idx >> 4, nseg = n >> 4;
-        out1[((seg & 1023) * (nseg >> 10) + (seg >> 10)) * 16 + (idx & 15)] = e.x;
-      }
-      else if (!(dbg & 1))
-        ((e.y >> 31) ? records : out1)[e.y & 0x7FFFFFFFu] = e.x;
-    }
-    __syncthreads();
-  }
-}
-
-// Ingest plan (one workgroup, after the tile totals are known):
-//   plan[0..FS]          level-2 item_start per super-tile (nb_j items of equal
-//                        slab ranges, ~B2_ITEM level-1 records each: skew-balanced;
-//                        0 items for a super-tile whose tiles are all split/empty)
-//   plan[FS+1 .. 2FS]    slab-range size per super-tile
-//   plan[2FS+1 .. 3FS]   hot non-split tiles of the super-tile (tile-in-ST, byte 0
-//                        and 1; 0xFF = none): >= 1/8 of its level-1 records
-//   plan[3FS+1 .. +NHOT] hot k_bin1 bins (>= 1/128 of all records, or ~0u)
-//   plan[PLAN_DBITS..]   this batch's direct tiles (bitmap, prefixes, list, split index)
-//   nxt                  the next batch's split set
-//   plan[PLAN_HINT..+1]  hot count columns for the next batch's k_count
-__global__ __launch_bounds__(1024) void k_stplan(uint32_t F, int G, const uint32_t* __restrict__ coltot,
-                                                 uint32_t* __restrict__ plan, const uint32_t* __restrict__ cur,
-                                                 uint32_t* __restrict__ nxt, uint32_t thr_min, uint32_t dmax,
-                                                 uint32_t split_min, int hot_bins, const uint32_t* __restrict__ err,
-                                                 uint32_t* __restrict__ err_host) {
-  // the invalid-id count of k_count, to the host's mapped pinned word (no copy launch)
-  if (threadIdx.x == 0) *reinterpret_cast<volatile uint32_t*>(err_host) = *err;
-  __shared__ uint4 lds4[17];
-  __shared__ unsigned long long best[16];
-  __shared__ uint32_t lhd[33], lhs[33];
-  __shared__ uint32_t sthr[2];
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t j = threadIdx.x;
-  const uint32_t NS = cur[0];
-  if (j < 33) lhd[j] = lhs[j] = 0;
-  __syncthreads();
-  // direct tiles: tiles of this batch (split or not: the exact totals of k_count)
-  // with >= max(thr_min, 2^k) records; next split set: tiles with >= max(split_min,
-  // 2^k) records
-  (void)NS;
-  {  // F <= 32768 tiles: a thread's <= 32 totals are loaded at once (one latency, not 32)
-    constexpr int PF = 32;
-    uint32_t tv[PF];
-#pragma unroll
-    for (int k = 0; k < PF; ++k) tv[k] = j + 1024u * k < F ? coltot[j + 1024u * k] : 0u;
-#pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      if (tv[k] >= split_min && tv[k] > 0) atomicAdd(&lhs[31 - __clz((int)tv[k])], 1u);
-      if (dmax > 0 && tv[k] >= thr_min && tv[k] > 0) atomicAdd(&lhd[31 - __clz((int)tv[k])], 1u);
-    }
-  }
-  __syncthreads();
-  if (j < 2) {
-    // cum_k = tiles with floor(log2 v) >= k (non-increasing in k): the smallest k
-    // with cum_k <= cap gives thr = max(lo, 2^k)
-    const uint32_t* lh = j ? lhs : lhd;
-    const uint32_t cap = j ? (uint32_t)SPLIT_MAX : dmax;
-    const uint32_t lo = max(j ? split_min : thr_min, 1u);
-    uint32_t thr = NOKEY;
-    if (cap > 0) {
-      uint32_t cum = 0;
-      int kbest = 32;
-      for (int k = 31; k >= 0; --k) {
-        cum += lh[k];
-        if (cum > cap) break;
-        kbest = k;
-      }
-      if (kbest < 32) thr = max(lo, 1u << kbest);
-    }
-    sthr[j] = thr;
-  }
-  __syncthreads();
-  const uint32_t thr_d = sthr[0], thr_s = sthr[1];
-  uint32_t nb = 0, gsz = 0, hot = 0xFFFFu, nn = 0, ndt = 0, n0 = 0, n1 = 0, d0 = 0, d1 = 0;
-  uint32_t c0 = 0, c1 = 0;  // this batch's split words of the super-tile
-  uint64_t ctot = 0, tot = 0;
-  unsigned long long tkA = 0, tkB = 0;  // (records << 16 | tile): this thread's two biggest tiles
-  if (j < FS) {
-    c0 = cur[SPLIT_BITS + 2 * j];
-    c1 = 2 * j + 1 < 1024 ? cur[SPLIT_BITS + 2 * j + 1] : 0u;
-    const uint32_t t1 = min(F, (j + 1) * ST_TILES);
-    uint32_t b0 = 0, b1 = 0, i0 = 0xFF, i1 = 0xFF;  // two biggest level-1 tiles of this super-tile
-    uint32_t a0 = 0, a1 = 0, k0 = 0xFF, k1 = 0xFF;  // two biggest tiles
-    // the super-tile's 64 totals in 16 loads issued at once (coltot holds F + COLS
-    // words, so the reads past F stay in bounds; those tiles are skipped)
-    uint32_t cv[ST_TILES];
-    const uint4* c4 = reinterpret_cast<const uint4*>(coltot + j * ST_TILES);
-#pragma unroll
-    for (int q = 0; q < ST_TILES / 4; ++q) {
-      const uint4 x = c4[q];
-      cv[4 * q] = x.x;
-      cv[4 * q + 1] = x.y;
-      cv[4 * q + 2] = x.z;
-      cv[4 * q + 3] = x.w;
-    }
-#pragma unroll
-    for (uint32_t tl = 0; tl < (uint32_t)ST_TILES; ++tl) {
-      if (j * ST_TILES + tl < t1) {
-        const uint32_t v = cv[tl];
-        tot += v;
-        if (v > a0) { a1 = a0; k1 = k0; a0 = v; k0 = tl; }
-        else if (v > a1) { a1 = v; k1 = tl; }
-        if (v >= thr_s) {
-          if (tl < 32) n0 |= 1u << tl; else n1 |= 1u << (tl - 32);
-        }
-        if (v >= thr_d) {  // direct: no level-1 records
-          if (tl < 32) d0 |= 1u << tl; else d1 |= 1u << (tl - 32);
-        } else {
-          ctot += v;
-          if (v > b0) { b1 = b0; i1 = i0; b0 = v; i0 = tl; }
-          else if (v > b1) { b1 = v; i1 = tl; }
-        }
-      }
-    }
-    nn = (uint32_t)(__popc(n0) + __popc(n1));
-    ndt = (uint32_t)(__popc(d0) + __popc(d1));
-    tkA = k0 != 0xFF ? (((unsigned long long)a0 << 16) | (j * ST_TILES + k0)) : 0ull;
-    tkB = k1 != 0xFF ? (((unsigned long long)a1 << 16) | (j * ST_TILES + k1)) : 0ull;
-    if ((uint64_t)b0 * 8 < ctot || b0 == 0) i0 = 0xFF;
-    if ((uint64_t)b1 * 8 < ctot || b1 == 0) i1 = 0xFF;
-    hot = (i0 == 0xFF ? 0xFFu : 2 * i0) | ((i1 == 0xFF ? 0xFFu : 2 * i1) << 8);  // k_bin2 keys (half 0)
-    if (ctot > 0) {
-      uint32_t want = (uint32_t)((ctot + B2_ITEM - 1) / B2_ITEM);
-      want = max(1u, min(want, (uint32_t)G));
-      gsz = ((uint32_t)G + want - 1) / want;
-      nb = ((uint32_t)G + gsz - 1) / gsz;
-    } else {
-      gsz = (uint32_t)G;
-    }
-  }
-  uint32_t sv3[4] = {nb, nn, ndt, 0u}, st3[4];
-  block_excl_scan4<1024>(sv3, lds4, st3);
-  const uint32_t e = sv3[0], ne = sv3[1], de = sv3[2];
-  const uint32_t total = st3[0], nnt = st3[1], ndtot = st3[2];
-  // this thread's NHOT biggest k_bin1 bins, descending: (records << 11 | bin)
-  unsigned long long bk[NHOT] = {};
-  auto push = [&](unsigned long long k) {
-#pragma unroll
-    for (int q = 0; q < NHOT; ++q)
-      if (k > bk[q]) {
-        const unsigned long long x = bk[q];
-        bk[q] = k;
-        k = x;
-      }
-  };
-  if (j < FS) {
-    plan[j] = e;
-    plan[FS + 1 + j] = gsz;
-    uint16_t* imap = reinterpret_cast<uint16_t*>(plan + PLAN_ITEMS);  // k_bin2: item -> super-tile, one load
-    for (uint32_t k = 0; k < nb; ++k) imap[e + k] = (uint16_t)j;
-    plan[2 * FS + 1 + j] = hot;
-    // this batch's direct tiles, their split index and half bins
-    plan[PLAN_DBITS + 2 * j] = d0;
-    plan[PLAN_DPRE + 2 * j] = de;
-    if (2 * j + 1 < 1024) {
-      plan[PLAN_DBITS + 2 * j + 1] = d1;
-      plan[PLAN_DPRE + 2 * j + 1] = de + (uint32_t)__popc(d0);
-    }
-    // (stores only: the half totals of the direct tiles are read below, one direct tile
-    // per thread, instead of as a chain of dependent loads in this loop)
-    uint32_t di = de;
-    for (int q = 0; q < 2; ++q) {
-      uint32_t w = q ? d1 : d0;
-      const uint32_t cw = q ? c1 : c0;
-      const uint32_t sp = cur[SPLIT_PRE + 2 * j + q];
-      while (w) {
-        const uint32_t b = (uint32_t)(__ffs((int)w) - 1);
-        w &= w - 1u;
-        plan[PLAN_DLIST + di] = j * ST_TILES + 32u * q + b;
-        // split index, or NOKEY: an unsplit direct tile (its two bins share its range)
-        plan[PLAN_DSI + di] = ((cw >> b) & 1u) ? sp + (uint32_t)__popc(cw & ((1u << b) - 1u)) : NOKEY;
-        ++di;
-      }
-    }
-    if (ctot && hot_bins) push((ctot << 11) | j);
-    // the next batch's split set
-    nxt[SPLIT_BITS + 2 * j] = n0;
-    nxt[SPLIT_PRE + 2 * j] = ne;
-    if (2 * j + 1 < 1024) {
-      nxt[SPLIT_BITS + 2 * j + 1] = n1;
-      nxt[SPLIT_PRE + 2 * j + 1] = ne + (uint32_t)__popc(n0);
-    }
-    uint32_t h = ne;
-    for (int q = 0; q < 2; ++q) {
-      uint32_t w = q ? n1 : n0;
-      while (w) {
-        const uint32_t tl = (uint32_t)(__ffs((int)w) - 1) + 32u * q;
-        w &= w - 1u;
-        nxt[SPLIT_LIST + h++] = j * ST_TILES + tl;
-      }
-    }
-  }
-  if (threadIdx.x == 0) {
-    plan[FS] = total;
-    plan[PLAN_ND] = ndtot;
-    nxt[0] = nnt;
-  }
-  __syncthreads();  // the direct list is written
-  for (uint32_t d = threadIdx.x; hot_bins && d < ndtot; d += 1024) {  // the direct tiles' half bins as hot-bin candidates
-    const uint32_t si = plan[PLAN_DSI + d];
-    if (si == NOKEY) {  // an unsplit direct tile: its records split between both bins by series bit 4
-      const unsigned long long h = coltot[plan[PLAN_DLIST + d]] / 2;
-      push((h << 11) | (FS + 2 * d));
-      push((h << 11) | (FS + 2 * d + 1));
-    } else {
-      push(((unsigned long long)coltot[F + 2 * si] << 11) | (FS + 2 * d));
-      push(((unsigned long long)coltot[F + 2 * si + 1] << 11) | (FS + 2 * d + 1));
-    }
-  }
-  // grand total, the hot bins and the two biggest tiles (block reductions)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  auto block_reduce = [&](unsigned long long v, bool is_max) -> unsigned long long {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      const unsigned long long o = __shfl_xor(v, d, 64);
-      v = is_max ? (o > v ? o : v) : v + o;
-    }
-    __syncthreads();
-    if (lane == 0) best[w] = v;
-    __syncthreads();
-    unsigned long long r = 0;
-    for (int q = 0; q < 16; ++q) r = is_max ? (best[q] > r ? best[q] : r) : r + best[q];
-    return r;
-  };
-  const unsigned long long grand = block_reduce(tot, false);
-  // (only the lane-private hot-slot variants of k_bin1 use them: 16 barriers saved otherwise)
-  unsigned long long ks[NHOT] = {};
-  int head = 0;  // this thread's first bin not yet selected
-  // the hottest bins: 2 for the ballot ranking; all NHOT for the lane-private-slot
-  // development variant (hot_bins bit 2) -- each is a block reduction
-  const int nh = (hot_bins & 4) ? NHOT : 2;
-  if (hot_bins) {
-#pragma unroll
-    for (int q = 0; q < NHOT; ++q) {
-      if (q >= nh) break;
-      unsigned long long mine = 0;
-#pragma unroll
-      for (int r = 0; r < NHOT; ++r)
-        if (r == head) mine = bk[r];
-      ks[q] = block_reduce(mine, true);
-      if (mine != 0 && mine == ks[q]) ++head;
-    }
-  }
-  const unsigned long long t1 = block_reduce(tkA, true);
-  const unsigned long long t2 = block_reduce(tkA == t1 ? tkB : tkA, true);
-  if (threadIdx.x == 0) {
-    // bins with >= 1/128 of the records: k_bin1 counts them in lane-private slots
-    // when the hottest one holds >= half of all records
-    for (int h = 0; h < NHOT; ++h) {
-      const uint64_t v = ks[h] >> 11;
-      plan[3 * FS + 1 + h] = (v > 0 && v * 128 >= grand) ? (uint32_t)(ks[h] & 2047u) : NOKEY;
-    }
-    plan[PLAN_HS] = grand > 0 && (ks[0] >> 11) * 2 >= grand ? 1u : 0u;  // k_bin1: ballot ranks
-    // next batch's k_count hints: the count columns of the two biggest tiles
-    // (both halves of a tile that will be split); aggregation only
-    uint32_t hkey[4] = {NOKEY, NOKEY, NOKEY, NOKEY};
-    int nh = 0;
-    const unsigned long long ts[2] = {t1, t2};
-    for (int q = 0; q < 2 && nh < 4; ++q) {
-      const uint64_t v = ts[q] >> 16;
-      if (v == 0 || v * 64 < grand) continue;
-      const uint32_t t = (uint32_t)(ts[q] & 0xFFFFu);
-      const uint32_t wd = nxt[SPLIT_BITS + (t >> 5)];  // written above by this workgroup
-      const uint32_t bit = 1u << (t & 31u);
-      if (wd & bit) {
-        const uint32_t si = nxt[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
-        hkey[nh++] = F + 2 * si;
-        hkey[nh++] = F + 2 * si + 1;
-      } else {
-        hkey[nh++] = t;
-      }
-    }
-    for (int h = 0; h < 4; ++h) plan[PLAN_HINT + h] = hkey[h];
-  }
-}
-
-// Level 2.  Item = (super-tile j, slab range [g0, g1)).  Its level-1 records are
-// one contiguous range; the records of tile t (of half h of t, for a split tile)
-// in that range go, in any order, to [tile_base[t] (+ half-0 total) + pre[g0][col],
-// ...) -- exactly where the per-(slab, tile) segments g0..g1-1 of the final
-// layout lie.  Keys: 2 x tile-in-ST + half (half 0 for an unsplit tile).
-constexpr int B2_KEYS = 2 * ST_TILES;
-constexpr size_t bin2_lds(int ch) { return (size_t)ch * 8 + 3 * B2_KEYS * 4 + 16; }
-template <int CH2, int B2_NT>
-__global__ __launch_bounds__(B2_NT) void k_bin2(const uint32_t* __restrict__ out1, uint32_t F, int G,
-                                                const uint32_t* __restrict__ pre,
-                                                const uint32_t* __restrict__ tile_base,
-                                                const uint32_t* __restrict__ coltot,
-                                                const uint32_t* __restrict__ split,
-                                                const uint32_t* __restrict__ plan, Tables tb,
-                                                uint32_t* __restrict__ records) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint2* stage = reinterpret_cast<uint2*>(smem);  // [CH2] sub-chunk sorted by key: {record, global index - stage index}
-  uint32_t* cur = smem + 2 * CH2;                 // [B2_KEYS] global write position of each key
-  uint32_t* cnt = cur + B2_KEYS;                  // [B2_KEYS] records of each key in this sub-chunk
-  uint32_t* off = cnt + B2_KEYS;                  // [B2_KEYS] their exclusive offsets in stage
-  uint32_t* seg = off + B2_KEYS;                  // [2]
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t C = F + COLS;
-  const uint32_t item = blockIdx.x;
-  // (both loads at once: entries past the batch's items are stale, never used)
-  const uint32_t nitems = plan[FS];
-  const uint32_t j = reinterpret_cast<const uint16_t*>(plan + PLAN_ITEMS)[item];
-  if (item >= nitems) return;
-  const uint32_t gsz = plan[FS + 1 + j];
-  const int g0 = (int)((item - plan[j]) * gsz);
-  const int g1 = min(G, g0 + (int)gsz);
-  const uint32_t hp = plan[2 * FS + 1 + j];
-  const uint32_t hot0 = (hp & 0xFFu) == 0xFFu ? NOKEY : (hp & 0xFFu);
-  const uint32_t hot1 = ((hp >> 8) & 0xFFu) == 0xFFu ? NOKEY : ((hp >> 8) & 0xFFu);
-  const uint32_t hk[2] = {hot0, hot1};
-  const uint32_t t0 = j * ST_TILES;
-  const uint32_t nt = min((uint32_t)ST_TILES, F - t0);
-  // split (and not direct) tiles of the super-tile: records keyed by half
-  const uint32_t sw0 = split[SPLIT_BITS + 2 * j] & ~plan[PLAN_DBITS + 2 * j];
-  const uint32_t sw1 = 2 * j + 1 < 1024 ? split[SPLIT_BITS + 2 * j + 1] & ~plan[PLAN_DBITS + 2 * j + 1] : 0u;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    uint32_t q0 = 0, q1 = 0, r0 = 0, r1 = 0;  // keys 2 lane, 2 lane + 1: pre[g0], pre[g1]
-    if ((uint32_t)lane < nt) {
-      const uint32_t t = t0 + lane;
-      const uint32_t bit = 1u << (t & 31u);
-      const bool direct = plan[PLAN_DBITS + (t >> 5)] & bit;
-      const uint32_t wd = split[SPLIT_BITS + (t >> 5)];
-      const uint32_t tb0 = tile_base[t];
-      if (direct) {  // its records never reach level 1
-        cur[2 * lane] = cur[2 * lane + 1] = tb0;
-      } else if (wd & bit) {
-        const uint32_t si = split[SPLIT_PRE + (t >> 5)] + (uint32_t)__popc(wd & (bit - 1u));
-        const uint32_t c0 = F + 2 * si;
-        q0 = pre[(size_t)g0 * C + c0];
-        q1 = pre[(size_t)g0 * C + c0 + 1];
-        r0 = g1 < G ? pre[(size_t)g1 * C + c0] : coltot[c0];
-        r1 = g1 < G ? pre[(size_t)g1 * C + c0 + 1] : coltot[c0 + 1];
-        cur[2 * lane] = tb0 + q0;
-        cur[2 * lane + 1] = tb0 + coltot[c0] + q1;
-      } else {
-        q0 = pre[(size_t)g0 * C + t];
-        r0 = g1 < G ? pre[(size_t)g1 * C + t] : (tile_base[t + 1] - tb0);
-        cur[2 * lane] = tb0 + q0;
-        cur[2 * lane + 1] = 0;
-      }
-    }
-    cnt[2 * lane] = cnt[2 * lane + 1] = 0;
-    uint32_t p0 = q0 + q1, p1 = r0 + r1;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      p0 += __shfl_xor(p0, d, 64);
-      p1 += __shfl_xor(p1, d, 64);
-    }
-    if (lane == 0) {
-      seg[0] = tile_base[t0] + p0;
-      seg[1] = tile_base[t0] + p1;
-    }
-  }
-  __syncthreads();
-  const uint32_t A = seg[0], B = seg[1];
-  const uint32_t A16 = A & ~3u;  // 16-B aligned start; lanes below A are masked off
-  constexpr int PT = CH2 / B2_NT;  // records per thread (groups of 4)
-  uint4 xn[PT / 4];                 // next sub-chunk, prefetched while this one is sorted and written
-#pragma unroll
-  for (int k = 0; k < PT / 4; ++k) {
-    const uint32_t base = A16 + 4 * (k * B2_NT + threadIdx.x);
-    xn[k] = base < B ? *reinterpret_cast<const uint4*>(out1 + base) : make_uint4(0u, 0u, 0u, 0u);
-  }
-  for (uint32_t c0 = A16; c0 < B; c0 += CH2) {
-    uint32_t rec[PT], kv[PT], rank[PT];
-    uint4 xc[PT / 4];
-#pragma unroll
-    for (int k = 0; k < PT / 4; ++k) {
-      xc[k] = xn[k];
-      const uint32_t nbase = c0 + CH2 + 4 * (k * B2_NT + threadIdx.x);  // out1 padded to a multiple of 4
-      xn[k] = nbase < B ? *reinterpret_cast<const uint4*>(out1 + nbase) : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int k = 0; k < PT / 4; ++k) {
-      const uint32_t base = c0 + 4 * (k * B2_NT + threadIdx.x);
-      const uint4 x = xc[k];
-      const uint32_t xv[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t idx = base + e;
-        const bool valid = idx >= A && idx < B;
-        const uint32_t r = xv[e];
-        const uint32_t tl = r >> 26;
-        const uint32_t sp = ((tl < 32 ? sw0 : sw1) >> (tl & 31u)) & 1u;
-        rec[4 * k + e] = r;  // records pass through unchanged (key order is all that changes)
-        kv[4 * k + e] = valid ? 2u * tl + (sp & (r >> 25)) : 0xFFFFFFFFu;
-      }
-    }
-    hot_rank_batch<2, PT>(cnt, kv, hk, rank);
-    __syncthreads();
-    if (threadIdx.x < 64) {  // exclusive scan of the 128 key counts (one wave, two per lane)
-      const uint32_t a = cnt[2 * threadIdx.x], b = cnt[2 * threadIdx.x + 1];
-      const uint32_t x = wave_incl_scan32(a + b) - (a + b);
-      off[2 * threadIdx.x] = x;
-      off[2 * threadIdx.x + 1] = x + a;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      if (kv[k] != 0xFFFFFFFFu) {
-        const uint32_t o = off[kv[k]];
-        const uint32_t pos = o + rank[k];
-        stage[pos] = make_uint2(rec[k], cur[kv[k]] - o);
-      }
-    }
-    const uint32_t total = off[B2_KEYS - 1] + cnt[B2_KEYS - 1];
-    __syncthreads();
     {
-      uint2 ev[PT];
-      const uint32_t w0 = (threadIdx.x >> 6) * (PT * 64) + (threadIdx.x & 63u);  // each wave: a contiguous PT x 64 range
-#pragma unroll
-      for (int k = 0; k < PT; ++k) ev[k] = stage[w0 + k * 64];
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const uint32_t i = w0 + k * 64;
-        if (i < total) records[ev[k].y + i] = ev[k].x;
+      uint32_t rb = INVALID;
+      if (rc) {
+        if (rold + rc <= rcapv) rb = rbase + rold;
+        else hdr[H_OV1] = 1u;  // this run is dropped; k_rfix1 has the batch redone with exact regions
       }
-    }
-    if (threadIdx.x < B2_KEYS) {
-      cur[threadIdx.x] += cnt[threadIdx.x];
-      cnt[threadIdx.x] = 0;
+      ocx[rb_bin].y = rb;
+      cnt[rb_bin] = 0;  // (every reader of the counts is past the barrier above)
     }
     __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (each wave a contiguous PT x 64 range)
+      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
+      const uint2 e = stage[i];
+      const uint2 o = ocx[e.y & 2047u];
+      if (o.y != INVALID) rec32[o.y + (i - o.x)] = e.x;
+    }
+    __syncthreads();
+  }
+  if (pass == 0 && bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
+}
+
+// ------------------------------------------------------------------------
+// After level 1 (one workgroup, thread = bin): exact bin totals, the direct keys'
+// ranges, and on an overflow exact regions for the redo pass.
+__global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict__ meta, const uint32_t* __restrict__ err,
+                                                uint32_t* __restrict__ err_host) {
+  __shared__ uint32_t lds[17];
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  if (threadIdx.x == 0) *reinterpret_cast<volatile uint32_t*>(err_host) = *err;  // to the host's mapped word
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t ND = hdr[H_ND];
+  const uint32_t TB = FS + 2 * ND;
+  const uint32_t ov = hdr[H_OV1];
+  const uint32_t b = threadIdx.x;
+  const uint32_t c = b < TB ? meta[L.bcnt() + b] : 0u;
+  meta[L.btot() + b] = c;
+  uint32_t tot;
+  const uint32_t nb = block_excl_scan<1024>(round_up(c, 4), lds, &tot);
+  const uint32_t base = ov ? nb : meta[L.bbase() + b];
+  if (b >= FS && b < TB) {
+    const uint32_t t = meta[L.dlist() + ((b - FS) >> 1)], h = (b - FS) & 1u;
+    meta[L.kbase() + 2 * t + h] = base;
+    meta[L.kcnt() + 2 * t + h] = c;
+  }
+  if (ov) {
+    meta[L.bbase() + b] = nb;
+    meta[L.bcap() + b] = round_up(c, 4);
+    meta[L.bcnt() + b] = 0u;
+  }
+  __syncthreads();  // every thread has read H_OV1
+  if (b == 0) {
+    hdr[H_REDO1] = ov;
+    hdr[H_OV1] = 0u;
+    if (ov) hdr[H_NOVR1] += 1u;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Level-2 plan, one workgroup: thread j owns the 64 keys of tiles [32 j, 32 j + 32)
+// and super-tile j's items.
+__global__ __launch_bounds__(1024) void k_rplan2(size_t n, uint32_t F, uint32_t* __restrict__ kest,
+                                                 const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
+                                                 size_t cap16, uint32_t pct) {
+  __shared__ uint64_t l64[17];
+  __shared__ uint32_t lds[17];
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
+  const bool exact = m == n;
+  const double s = m ? (double)n / (double)m : 1.0;
+  const uint32_t j = threadIdx.x, t0 = j * 32;
+  const uint32_t dbits = t0 < F ? meta[L.dbits() + j] : 0u;
+  auto key_cap = [&](uint32_t k) -> uint32_t {  // this thread's key 2 t0 + k (0 for direct tiles)
+    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
+    if (t >= F || ((dbits >> (k >> 1)) & 1u)) return 0u;
+    return rcap((double)kprev[key], (double)kest[key], s, exact, 32.0, 8, pct);
+  };
+  uint64_t sum = 0;
+  for (uint32_t k = 0; k < 64; ++k) sum += key_cap(k);
+  uint64_t total;
+  uint64_t base = block_excl_scan64(sum, l64, &total);
+  double f = 1.0;
+  if (total + 64 > cap16) {  // too big for the buffer: scale down (an overflow is redone exactly)
+    f = (double)(cap16 - 64) / (double)total;
+    sum = 0;
+    for (uint32_t k = 0; k < 64; ++k) sum += (uint32_t)((double)key_cap(k) * f) & ~7u;
+    base = block_excl_scan64(sum, l64, &total);
+  }
+  for (uint32_t k = 0; k < 64; ++k) {
+    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
+    if (t >= F) break;
+    uint32_t c = key_cap(k);
+    if (f != 1.0) c = (uint32_t)((double)c * f) & ~7u;
+    if (!((dbits >> (k >> 1)) & 1u)) {
+      meta[L.kbase() + key] = (uint32_t)base;
+      meta[L.kcap() + key] = c;
+      meta[L.kcnt() + key] = 0u;
+    }
+    if (kest[key]) kest[key] = 0;  // ready for the next batch
+    base += c;
+  }
+  // level-2 items of super-tile j
+  const uint32_t tot = j < FS ? meta[L.btot() + j] : 0u;
+  const uint32_t ni = (tot + ITEM2 - 1) / ITEM2;
+  uint32_t all;
+  const uint32_t is = block_excl_scan<1024>(ni, lds, &all);
+  uint16_t* imap = reinterpret_cast<uint16_t*>(meta + L.imap());
+  if (j < FS) {
+    meta[L.istart() + j] = is;
+    for (uint32_t q = 0; q < ni; ++q) imap[is + q] = (uint16_t)j;
+  }
+  if (j == 0) {
+    meta[L.istart() + FS] = all;
+    hdr[H_ITEMS] = all;
+    hdr[H_OV2] = 0u;
+    hdr[H_REDO2] = 0u;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Level 2 (persistent): workgroup w walks items [w I / G, (w + 1) I / G) -- item
+// order is super-tile order, so a workgroup sees few super-tiles and folds the
+// value sums of one super-tile's 2048 series in LDS (u64), flushed to sumfix when
+// it moves on.  Per item (<= ITEM2 level-1 records, 16 per thread): bucket (LUT),
+// 16-bit record, key = 2 tile-in-ST + half; LDS counting sort by key, one returning
+// global atomic per non-empty key on its cursor, stage {rec16 | key << 16}, written
+// in order to run base + position.
+constexpr int B2_KEYS = 2 * ST_TILES;
+constexpr size_t rbin2_lds() { return (size_t)ITEM2 * 4 + 2048 * 8 + LUT2_N * 8 + B2_KEYS * 12 + 16; }
+
+template <int NT>
+__global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
+                                                 const uint32_t* __restrict__ rec32, uint16_t* __restrict__ rec16,
+                                                 int64_t* __restrict__ sumfix, int pass) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* stage = smem;                                                             // [ITEM2]
+  unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem + ITEM2);     // [2048]
+  uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                                // [LUT2_N]
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);                         // [B2_KEYS]
+  uint2* ocx = reinterpret_cast<uint2*>(cnt + B2_KEYS);                               // [B2_KEYS]
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO2]) == 0u) return;
+  const uint32_t nitems = hdr[H_ITEMS];
+  const uint32_t i0 = (uint32_t)(((uint64_t)blockIdx.x * nitems) / gridDim.x);
+  const uint32_t i1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * nitems) / gridDim.x);
+  if (i0 >= i1) return;
+  const uint16_t* imap = reinterpret_cast<const uint16_t*>(meta + L.imap());
+  uint32_t* kcnt = meta + L.kcnt();
+  const uint32_t* kbase = meta + L.kbase();
+  const uint32_t* kcap = meta + L.kcap();
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+  for (int i = threadIdx.x; i < 2048; i += NT) lsum[i] = 0ull;
+  for (int i = threadIdx.x; i < B2_KEYS; i += NT) cnt[i] = 0u;
+  uint32_t cur_j = 0xFFFFFFFFu;
+  auto flush = [&](uint32_t jj) {  // the super-tile's value sums into sumfix (one atomic per nonzero series)
+    for (int i = threadIdx.x; i < 2048; i += NT) {
+      const unsigned long long v = lsum[i];
+      const uint32_t s = jj * 2048u + (uint32_t)i;
+      if (v && s < S) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), v);
+      lsum[i] = 0ull;
+    }
+  };
+  constexpr int PG = ITEM2 / 4 / NT;  // 16-B groups per thread
+  for (uint32_t item = i0; item < i1; ++item) {
+    const uint32_t j = imap[item];
+    const uint32_t q = item - meta[L.istart() + j];
+    const uint32_t a = meta[L.bbase() + j] + q * ITEM2;  // 4-aligned
+    const uint32_t e = min(a + ITEM2, meta[L.bbase() + j] + meta[L.btot() + j]);
+    uint4 x[PG];
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x);
+      x[g] = idx < e ? *reinterpret_cast<const uint4*>(rec32 + idx) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (j != cur_j) {
+      __syncthreads();  // the previous item's write-out has read the stage
+      if (pass == 0 && cur_j != 0xFFFFFFFFu) flush(cur_j);
+      cur_j = j;
+      __syncthreads();
+    }
+    // {rec16 | key << 16} of slot k of group g (~0u: no record); decoded twice -- here
+    // for the ranks and the sums, after the scan for the stage -- to keep the
+    // records (x) and ranks in registers without spilling
+    auto decode = [&](int g, int k, uint32_t r, bool sums) -> uint32_t {
+      const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x) + (uint32_t)k;
+      const uint32_t p = r & 0x1FFFFFu;
+      uint32_t o;
+      const uint32_t b = lut2_decode(p, lut2[lut2_index(p)], o);
+      const bool esc = p >= V_ESC;
+      const uint32_t bucket = sel_u32(esc, p - V_ESC, b);
+      const uint32_t sl = (r >> 21) & 31u, tl = r >> 26;
+      if (idx >= e) return NOKEY;
+      if (sums && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
+      return (sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16);
+    };
+    uint32_t rank[4 * PG];
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t kr = decode(g, k, xs[k], pass == 0);
+        rank[4 * g + k] = kr != NOKEY ? atomicAdd(&cnt[kr >> 16], 1u) : 0u;
+      }
+    }
+    __syncthreads();
+    // run reservations: waves 0 and 1, lane = key; wave 0 also scans the key counts
+    uint32_t rc = 0, rold = 0, rbase = 0, rcapv = 0;
+    const uint32_t rk = (uint32_t)wv * 64u + (uint32_t)lane;
+    const uint32_t gk = j * (uint32_t)B2_KEYS + rk;
+    if (wv < 2) {
+      rc = cnt[rk];
+      if (rc) {
+        rold = atomicAdd(&kcnt[gk], rc);
+        rbase = kbase[gk];
+        rcapv = kcap[gk];
+      }
+    }
+    if (wv == 0) {
+      const uint32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
+      const uint32_t ex = wave_incl_scan32(c0 + c1) - (c0 + c1);
+      ocx[2 * lane].x = ex;
+      ocx[2 * lane + 1].x = ex + c0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t kr = decode(g, k, xs[k], false);
+        if (kr != NOKEY) stage[ocx[kr >> 16].x + rank[4 * g + k]] = kr;
+      }
+    }
+    if (wv < 2) {
+      uint32_t rb = INVALID;
+      if (rc) {
+        if (rold + rc <= rcapv) rb = rbase + rold;
+        else hdr[H_OV2] = 1u;  // dropped; k_rfix2 has level 2 redone with exact regions
+      }
+      ocx[rk].y = rb;
+      cnt[rk] = 0u;
+    }
+    __syncthreads();
+    const uint32_t total = e - a;
+#pragma unroll
+    for (int k = 0; k < 4 * PG; ++k) {  // each wave a contiguous range of the stage
+      const uint32_t i = (uint32_t)wv * (4 * PG * 64) + (uint32_t)k * 64 + (uint32_t)lane;
+      if (i < total) {
+        const uint32_t v = stage[i];
+        const uint2 o = ocx[v >> 16];
+        if (o.y != INVALID) rec16[o.y + (i - o.x)] = (uint16_t)(v & 0xFFFFu);
+      }
+    }
+  }
+  __syncthreads();
+  if (pass == 0) flush(cur_j);
+}
+
+// After level 2 (one workgroup; thread j owns the 64 keys of tiles [32 j, 32 j + 32)):
+// the exact key counts become the next batch's prediction; on an overflow, exact
+// regions for the redo pass.
+__global__ __launch_bounds__(1024) void k_rfix2(uint32_t F, uint32_t* __restrict__ meta, uint32_t* __restrict__ kprev) {
+  __shared__ uint64_t l64[17];
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  const uint32_t ov = hdr[H_OV2];
+  const uint32_t j = threadIdx.x, t0 = j * 32;
+  const uint32_t dbits = t0 < F ? meta[L.dbits() + j] : 0u;
+  uint64_t sum = 0;
+  for (uint32_t k = 0; k < 64; ++k) {
+    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
+    if (t >= F) break;
+    const uint32_t x = meta[L.kcnt() + key];
+    kprev[key] = x;
+    if (!((dbits >> (k >> 1)) & 1u)) sum += round_up(x, 8);
+  }
+  if (ov) {  // (block-uniform)
+    uint64_t total;
+    uint64_t base = block_excl_scan64(sum, l64, &total);
+    for (uint32_t k = 0; k < 64; ++k) {
+      const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
+      if (t >= F) break;
+      if (!((dbits >> (k >> 1)) & 1u)) {
+        const uint32_t c8 = round_up(meta[L.kcnt() + key], 8);
+        meta[L.kbase() + key] = (uint32_t)base;
+        meta[L.kcap() + key] = c8;
+        meta[L.kcnt() + key] = 0u;
+        base += c8;
+      }
+    }
+  }
+  __syncthreads();
+  if (j == 0) {
+    hdr[H_REDO2] = ov;
+    hdr[H_OV2] = 0u;
+    if (ov) hdr[H_NOVR2] += 1u;
   }
 }
 
@@ -1123,6 +756,8 @@ __global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__
   }
 }
 
+constexpr int CH1 = 16384;
+
 }  // namespace
 
 hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
@@ -1133,125 +768,43 @@ hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* d
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------
 hipError_t set_ingest_attributes() {
   hipError_t e;
-  const int big = 160 * 1024;
-  if ((e = hipFuncSetAttribute((const void*)k_count, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin, hipFuncAttributeMaxDynamicSharedMemorySize, big))) return e;
-  if ((e = hipFuncSetAttribute((const void*)k_tilescan_seg, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)((tpad(32768) + 1) * 4))))
+  if ((e = hipFuncSetAttribute((const void*)k_rsample, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4)))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bin1_lds(16384))))
+  if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1_lds(CH1))))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<6144, 512, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bin1_lds(6144))))
-    return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin1<16384, 1024, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bin1_lds(16384))))
-    return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin2<8192, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bin2_lds(8192))))
-    return e;
-  if ((e = hipFuncSetAttribute((const void*)k_bin2<16384, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bin2_lds(16384))))
-    return e;
-
-
-  return hipSuccess;
+  return hipFuncSetAttribute((const void*)k_rbin2<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
 }
 
-hipError_t launch_count(const uint32_t* series, size_t n, size_t per, int G, uint32_t S, uint32_t F,
-                        uint32_t* table, uint32_t* err, const uint32_t* hint, const uint32_t* split, bool vec,
-                        hipStream_t st) {
-  hipLaunchKernelGGL(k_count, dim3(G), dim3(WG), ((size_t)F + COLS + 2048) * 4, st, series, n, per, S, F, table, err,
-                     hint, split, vec ? 1 : 0);
-  return hipGetLastError();
-}
-
-hipError_t launch_colscan(uint32_t* table, int G, uint32_t F, uint32_t* coltot, hipStream_t st) {
-  hipLaunchKernelGGL(k_colscan, dim3((F + COLS + 63) / 64), dim3(1024), 0, st, table, G, F + COLS, coltot);
-  return hipGetLastError();
-}
-
-hipError_t launch_tilescan(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base, hipStream_t st) {
-  hipLaunchKernelGGL(k_tilescan, dim3(1), dim3(1024), 0, st, coltot, F, split, tile_base);
-  return hipGetLastError();
-}
-
-hipError_t launch_tilescan_seg(uint32_t* coltot, uint32_t F, const uint32_t* split, uint32_t* tile_base,
-                               uint32_t* sinfo, hipStream_t st) {
-  hipLaunchKernelGGL(k_tilescan_seg, dim3(1), dim3(1024), (tpad(F) + 1) * 4, st, coltot, F, split, tile_base, sinfo);
-  return hipGetLastError();
-}
-
-hipError_t launch_seginfo(const uint32_t* split, const uint32_t* coltot, uint32_t F, uint32_t* sinfo, hipStream_t st) {
-  hipLaunchKernelGGL(k_seginfo, dim3(1), dim3(1024), 0, st, split, coltot, F, sinfo);
-  return hipGetLastError();
-}
-
-hipError_t launch_encode1(const uint32_t* series, const float* values, size_t n, uint32_t S, Tables tb,
-                          uint32_t* records, int64_t* sumfix, uint32_t* tile_base, uint32_t* err, bool vec, int num_cu,
-                          hipStream_t st) {
-  const size_t groups = (n + 4 * 256 - 1) / (4 * 256);
-  const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(groups, (size_t)num_cu * 8));
-  hipLaunchKernelGGL(k_encode1, dim3(grid), dim3(256), 0, st, series, values, n, S, tb, records, sumfix, tile_base, err,
-                     vec ? 1 : 0);
-  return hipGetLastError();
-}
-
-hipError_t launch_bin(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
-                      uint32_t F, const uint32_t* table, const uint32_t* tile_base, Tables tb, uint32_t* records,
-                      int64_t* sumfix, bool vec, hipStream_t st) {
-  const size_t lds = (size_t)F * 4;  // the batch was counted without split tiles (tile columns only)
-  hipLaunchKernelGGL(k_bin, dim3(G), dim3(WG), lds, st, series, values, n, per, S, F, table, tile_base, tb, records,
-                     sumfix, vec ? 1 : 0);
-  return hipGetLastError();
-}
-
-hipError_t launch_stplan(uint32_t F, int G, const uint32_t* coltot, uint32_t* stplan, const uint32_t* cur,
-                         uint32_t* nxt, uint32_t thr_min, uint32_t dmax, uint32_t split_min, int hot_bins,
-                         const uint32_t* err, uint32_t* err_host, hipStream_t st) {
-  const uint32_t FS = (F + 63) / 64;
-  const uint32_t cap = std::min<uint32_t>((uint32_t)DIRECT_MAX, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + trash bin
-  hipLaunchKernelGGL(k_stplan, dim3(1), dim3(1024), 0, st, F, G, coltot, stplan, cur, nxt, thr_min, std::min(dmax, cap),
-                     split_min, hot_bins, err, err_host);
-  return hipGetLastError();
-}
-
-hipError_t launch_bin1(const uint32_t* series, const float* values, size_t n, size_t per, int G, uint32_t S,
-                       uint32_t F, const uint32_t* pre, const uint32_t* tile_base, Tables tb, const uint32_t* stplan,
-                       const uint32_t* coltot, const uint32_t* split, uint32_t* scratch1, uint32_t* records,
-                       int64_t* sumfix, bool vec, int dbg, hipStream_t st) {
-  // sub-chunk size x workgroup: (16384 slots, 1024 threads, 1 workgroup/CU) by
-  // default -- longer runs per bin beat the second workgroup's overlap (measured);
-  // L5DH_DBG bit 20 selects (6144, 512, 2 workgroups/CU)
-  if ((dbg >> 20) & 1)
-    hipLaunchKernelGGL((k_bin1<6144, 512, 4, true>), dim3(G), dim3(512), bin1_lds(6144), st, series, values, n, per, S, F,
-                       pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
-  else if ((dbg >> 22) & 1)  // bit 22: lane-private slots for the hottest bins (measured 5-8 % slower)
-    hipLaunchKernelGGL((k_bin1<16384, 1024, 4, true>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
-                       F, pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
-  else
-    hipLaunchKernelGGL((k_bin1<16384, 1024, 4, false>), dim3(G), dim3(1024), bin1_lds(16384), st, series, values, n, per, S,
-                       F, pre, tile_base, tb, stplan, coltot, split, scratch1, records, sumfix, vec ? 1 : 0, dbg);
-  return hipGetLastError();
-}
-
-hipError_t launch_bin2(const uint32_t* scratch1, size_t n, int G, uint32_t F, const uint32_t* pre,
-                       const uint32_t* tile_base, const uint32_t* coltot, const uint32_t* split, Tables tb,
-                       const uint32_t* stplan, uint32_t* records, int dbg, hipStream_t st) {
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const size_t max_items = n / B2_ITEM + FS + 1;  // sum_j ceil(tot_j / B2_ITEM)
-  // sub-chunk x workgroup: (8192, 512) by default (measured: longer runs per key
-  // than (4096, 256)); L5DH_DBG bit 21: (16384, 1024)
-  if ((dbg >> 21) & 1)
-    hipLaunchKernelGGL((k_bin2<16384, 1024>), dim3((unsigned)max_items), dim3(1024), bin2_lds(16384), st, scratch1, F,
-                       G, pre, tile_base, coltot, split, stplan, tb, records);
-  else
-    hipLaunchKernelGGL((k_bin2<8192, 512>), dim3((unsigned)max_items), dim3(512), bin2_lds(8192), st, scratch1, F, G,
-                       pre, tile_base, coltot, split, stplan, tb, records);
+hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
+  const uint32_t K = 2 * a.F;
+  switch (stage) {
+    case 0:  // sample + level-1 plan
+      hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
+                         a.kest);
+      hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32, a.thr_min,
+                         a.dmax, a.pct);
+      break;
+    case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
+      for (int pass = 0; pass < 2; ++pass) {
+        hipLaunchKernelGGL((k_rbin1<CH1, 1024>), dim3(a.G), dim3(1024), rbin1_lds(CH1), st, a.series, a.values, a.n,
+                           a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+        if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);
+      }
+      break;
+    case 2:  // level-2 plan
+      hipLaunchKernelGGL(k_rplan2, dim3(1), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap16, a.pct);
+      break;
+    default:  // level 2, its fix-up, the redo pass
+      for (int pass = 0; pass < 2; ++pass) {
+        hipLaunchKernelGGL(k_rbin2<1024>, dim3(a.num_cu), dim3(1024), rbin2_lds(), st, a.S, a.F, a.tb, a.meta, a.rec32,
+                           a.rec16, a.sumfix, pass);
+        if (pass == 0) hipLaunchKernelGGL(k_rfix2, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.kprev);
+      }
+      break;
+  }
   return hipGetLastError();
 }
 

@@ -1,0 +1,157 @@
+// l5dh_merge.hip -- the fleet merge's sparse exchange (l5dh_merge, config C4).
+//
+// A rank's exported dense rows [Sp][1798] (int32 counts) are mostly zeros (C4: a
+// rank holds ~125 samples per series), so the reduce-scatter does not move them
+// dense.  Each row is encoded as its non-empty buckets in bucket order, one u32
+// per bucket: bucket << 21 | count (count < 2^21 - 1), or bucket << 21 | 0x1FFFFF
+// followed by the count's full 32 bits.  A rank sends each other rank the encoding
+// of that rank's row slice plus the words per row; the receiver adds the sources'
+// entries into LDS rows (one wave per series; a source holds each bucket once, the
+// sources are added in rank order -- integer sums, bit-exact), writes the summed
+// dense row and summarizes it in the same pass.
+//
+//   k_mcount   words per row
+//   k_menc     the rows' entries at their exclusive word offsets
+//   k_mdecode  summed rows of this rank's slice from every source + HistogramSummary
+#include <hipcub/hipcub.hpp>
+
+#include "l5dh_device.hpp"
+#include "l5dh_merge.hpp"
+
+namespace l5dh {
+namespace {
+
+constexpr uint32_t CMAX = 0x1FFFFFu;  // count field; CMAX marks an escaped count
+
+__global__ __launch_bounds__(256) void k_mcount(const int32_t* __restrict__ rows, uint32_t nrows,
+                                                uint32_t* __restrict__ words) {
+  const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int lane = lane_id();
+  const int32_t* row = rows + (size_t)r * NB;
+  uint32_t w = 0;
+  for (int b = lane; b < NB; b += 64) {
+    const uint32_t c = (uint32_t)row[b];
+    w += (c != 0u) + (c >= CMAX);
+  }
+  w = (uint32_t)wave_sum((uint64_t)w);
+  if (lane == 0) words[r] = w;
+}
+
+__global__ __launch_bounds__(256) void k_menc(const int32_t* __restrict__ rows, uint32_t nrows,
+                                              const uint64_t* __restrict__ offs, uint32_t* __restrict__ enc) {
+  const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int lane = lane_id();
+  const int32_t* row = rows + (size_t)r * NB;
+  uint64_t at = offs[r];
+  for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 buckets per step, compacted by ballots
+    const int b = b0 + lane;
+    const uint32_t c = b < NB ? (uint32_t)row[b] : 0u;
+    const bool nz = c != 0u, esc = c >= CMAX;
+    const unsigned long long mn = __ballot(nz), me = __ballot(esc);
+    const uint32_t pos = mask_below(mn) + mask_below(me);
+    if (nz) {
+      enc[at + pos] = ((uint32_t)b << 21) | (esc ? CMAX : c);
+      if (esc) enc[at + pos + 1] = c;
+    }
+    at += (uint64_t)(__popcll(mn) + __popcll(me));
+  }
+}
+
+// One wave per series of the slice: the LDS row accumulates every source's entries
+// (a source's words are parsed 64 at a time; escape headers are rare, resolved by a
+// loop over their ballot), then the dense row, the total and the summary.
+constexpr int MDEC_WAVES = 4;
+__global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeSources src, uint32_t nrows,
+                                                             const int64_t* __restrict__ totals, Tables tb,
+                                                             int32_t* __restrict__ out_rows,
+                                                             Summary88* __restrict__ out_summ) {
+  __shared__ __attribute__((aligned(16))) uint32_t lrow[MDEC_WAVES][ROW];
+  const int w = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const uint32_t r = blockIdx.x * MDEC_WAVES + w;
+  if (r >= nrows) return;  // (wave-uniform; no barriers below)
+  uint32_t* row = lrow[w];
+  for (int b = lane; b < ROW; b += 64) row[b] = 0u;
+  for (int s = 0; s < src.n; ++s) {
+    const uint32_t* enc = src.enc[s] + src.offs[s][r];
+    const uint32_t nw = src.words[s][r];
+    bool carry = false;  // the chunk's first word is the count of the previous chunk's last header
+    for (uint32_t base = 0; base < nw; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      const bool valid = i < nw;
+      const uint32_t x = valid ? enc[i] : 0u;
+      unsigned long long hm = __ballot(valid && (x & CMAX) == CMAX);  // escape headers, or counts that look like one
+      unsigned long long pay = 0ull;
+      if (carry) {
+        pay |= 1ull;
+        hm &= ~1ull;
+      }
+      bool next_carry = false;
+      while (hm) {  // headers in order: the word after a header is its count, never a header
+        const int h = __ffsll((long long)hm) - 1;
+        hm &= ~(1ull << h);
+        if (h == 63) {
+          next_carry = true;
+        } else {
+          pay |= 1ull << (h + 1);
+          hm &= ~(1ull << (h + 1));
+        }
+      }
+      const uint32_t nxt = __shfl_down(x, 1, 64);
+      if (valid && !((pay >> lane) & 1ull)) {
+        const uint32_t b = x >> 21;
+        uint32_t c = x & CMAX;
+        if (c == CMAX) c = lane == 63 ? enc[i + 1] : nxt;
+        row[b] += c;  // one wave owns the row; a source holds each bucket once
+      }
+      carry = next_carry;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const SrcLds32 lds{row};
+  uint32_t g[9];
+  if (out_rows) {
+    int32_t* orow = out_rows + (size_t)r * NB;
+    for (int q = lane; q < NB4; q += 64) store4_1798(orow, 4 * q, lds.get4(4 * q));
+  }
+  const int ng = lane_groups(lane);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
+  wave_summary(g, lds, totals ? totals[r] : 0, tb.mid, out_summ ? out_summ + r : nullptr);
+}
+
+}  // namespace
+
+hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
+                       size_t* tmp_bytes, hipStream_t st) {
+  if (!tmp) {  // size query of the scan's temporary storage
+    return hipcub::DeviceScan::ExclusiveSum(nullptr, *tmp_bytes, words, offs, (int)nrows + 1, st);
+  }
+  if (nrows) hipLaunchKernelGGL(k_mcount, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, words);
+  hipError_t e = hipMemsetAsync(words + nrows, 0, 4, st);  // offs[nrows] = the total
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, words, offs, (int)nrows + 1, st);
+}
+
+hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_menc, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, offs, enc);
+  return hipGetLastError();
+}
+
+hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
+                         hipStream_t st) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, words, offs, (int)nrows, st);
+}
+
+hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
+                        Summary88* out_summ, hipStream_t st) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mdecode, dim3((nrows + MDEC_WAVES - 1) / MDEC_WAVES), dim3(64 * MDEC_WAVES), 0, st, src, nrows,
+                     totals, tb, out_rows, out_summ);
+  return hipGetLastError();
+}
+
+}  // namespace l5dh

@@ -1,0 +1,30 @@
+// l5dh_merge.hpp -- the fleet merge's sparse row exchange (l5dh_merge.hip).
+#pragma once
+
+#include "l5dh_kernels.hpp"
+
+namespace l5dh {
+
+constexpr int MERGE_MAX_RANKS = 64;
+
+struct MergeSources {  // the encodings of this rank's row slice, one per source rank
+  const uint32_t* enc[MERGE_MAX_RANKS];    // entries
+  const uint32_t* words[MERGE_MAX_RANKS];  // [nrows] words per row
+  const uint64_t* offs[MERGE_MAX_RANKS];   // [nrows] exclusive offsets of the rows' words
+  int n;
+};
+
+// words[r] = entry words of row r (words needs nrows + 1 slots), offs[0..nrows] their
+// exclusive prefix (offs[nrows] = the total).  tmp == nullptr: *tmp_bytes receives the
+// scan's temporary storage size.
+hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
+                       size_t* tmp_bytes, hipStream_t st);
+hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st);
+// offs[0..nrows) = exclusive prefix of words (a received slice); tmp from merge_count's query
+hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
+                         hipStream_t st);
+// summed rows of the slice (out_rows nullable: [nrows][1798]) and their summaries
+hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
+                        Summary88* out_summ, hipStream_t st);
+
+}  // namespace l5dh

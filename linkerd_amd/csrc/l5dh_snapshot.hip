@@ -1,133 +1,61 @@
 // l5dh_snapshot.hip -- snapshot-side kernels (Metric.Stat.snapshot/reset/summary,
 // batched as AdminMetricsExportTelemeter.snapshotHistograms drives them).
 //
-//   k_plan       per tile: records over pending segments, cold/hot, work items
-//   k_hot_init   zero the state rows of clean hot tiles
-//   k_accum      cold tile: 32 series in u16-packed LDS bins, fused summary +
-//                dense flush; hot tile: (half, chunk) partial in u32 LDS bins,
-//                flushed with global atomics
-//   k_hot_finish summaries of hot tiles from their merged state rows
-//   k_rows       summaries / dense copies of state rows or external rows
+//   k_plan_a/b     per tile: records over pending segments, cold/big, work items
+//   k_hot_init     zero the rows big tiles accumulate into
+//   k_accum_cold_p cold tile: 32 series in u16-packed LDS bins, fused summary +
+//                  dense flush (persistent)
+//   k_accum_split  big half-tile: (half, chunk) partial in u32 LDS bins, flushed
+//                  with global atomics (persistent)
+//   k_hot_finish   summaries of big tiles from their merged rows
+//   k_rows         summaries / dense copies of state rows or external rows
+//   k_fold1        one-tile series spaces folded into state rows at ingest
+//
+// Every (tile, half) key of a segment is one contiguous range (l5dh_kernels.hpp):
+// rec32 level-1 records of a direct tile (payload: value or escaped bucket), or
+// rec16 level-2 records (series in tile | bucket; their value sums are in sumfix).
 #include "l5dh_device.hpp"
-// L5DH_EXP (compile time, tools/mk_var.sh): timing-only variants, results invalid.
-//   1 k_accum_split without the value-sum atomics, 2 without the bin atomics
-#ifndef L5DH_EXP
-#define L5DH_EXP 0
-#endif
 
 namespace l5dh {
 namespace {
 
-__constant__ int g_dbg;  // L5DH_DBG timing-only variants (results invalid): 0x100 no records, 0x200 no dense stores
-int g_dbg_host = 0;      // host copy of L5DH_DBG (launch-time variants)
-
-// k_plan: one workgroup.  Per tile: records across segments, hot/cold, work
-// items; exclusive scans -> cold_tile[] (item -> tile), hot_item[] (item -> tile
-// and chunk), hot_list, header {cold items, multi-chunk tiles, hot items}.
-__global__ __launch_bounds__(1024) void k_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
-                                               uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
-  __shared__ uint32_t lds_a[17];
-  __shared__ uint32_t lds_b[17];
-  __shared__ uint32_t lds_c[17];
-  __shared__ uint32_t lds_d[17];
-  const uint32_t per = (F + 1023) / 1024;
-  const uint32_t t0 = threadIdx.x * per;
-  // cold items, mixed-half chunk items, big tiles, split items
-  uint32_t ci = 0, hi = 0, hot = 0, si = 0;
-  // a big tile is accumulated per half when it is split in every pending segment:
-  // returns its half-0 records across the segments (or ~0u)
-  auto split_h0 = [&](uint32_t t) -> uint32_t {
-    if (segs.n == 0) return 0xFFFFFFFFu;
-    uint32_t h0 = 0;
-    for (int j = 0; j < segs.n; ++j) {
-      const uint16_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
-      if (m == NO_SPLIT) return 0xFFFFFFFFu;
-      h0 += segs.sinfo[j][SINFO_H0 + m];
-    }
-    return h0;
-  };
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t t = t0 + k;
-    if (t >= F) break;
-    uint32_t tot = 0;
-    for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
-    plan.tile_tot[t] = tot;
-    if (tot > cold_limit) {
-      hot += 1;
-      const uint32_t h0 = split_h0(t);
-      if (h0 != 0xFFFFFFFFu)
-        si += (h0 + hot_chunk - 1) / hot_chunk + (tot - h0 + hot_chunk - 1) / hot_chunk;
-      else
-        hi += (tot + hot_chunk - 1) / hot_chunk;
-    } else if (final_mode || tot > 0) {
-      ci += 1;
-    }
-  }
-  uint32_t tot_c, tot_h, tot_hot, tot_s;
-  uint32_t ca = block_excl_scan<1024>(ci, lds_a, &tot_c);
-  uint32_t ha = block_excl_scan<1024>(hi, lds_b, &tot_h);
-  uint32_t xa = block_excl_scan<1024>(hot, lds_c, &tot_hot);
-  uint32_t sa = block_excl_scan<1024>(si, lds_d, &tot_s);
-  for (uint32_t k = 0; k < per; ++k) {
-    const uint32_t t = t0 + k;
-    if (t >= F) break;
-    const uint32_t tot = plan.tile_tot[t];
-    uint8_t flags = dirty[t] ? TF_DIRTY : 0;
-    if (tot > cold_limit) {
-      const uint32_t h0 = split_h0(t);
-      if (h0 != 0xFFFFFFFFu) {
-        flags |= TF_SPLIT;
-        for (uint32_t h = 0; h < 2; ++h) {
-          const uint32_t nh = ((h ? tot - h0 : h0) + hot_chunk - 1) / hot_chunk;
-          for (uint32_t c = 0; c < nh; ++c) plan.split_item[sa++] = make_uint2(t | (h << 15), c);
-        }
-      } else {
-        const uint32_t nc = (tot + hot_chunk - 1) / hot_chunk;
-        for (uint32_t c = 0; c < nc; ++c) plan.hot_item[ha + c] = t | (c << 15);
-        ha += nc;
-      }
-      plan.hot_list[xa++] = t;
-    } else if (final_mode || tot > 0) {
-      plan.cold_tile[ca++] = t;
-    }
-    plan.tile_flags[t] = flags;
-  }
-  if (threadIdx.x == 0) {
-    const uint32_t h[4] = {tot_c, tot_hot, tot_h, tot_s};
-    for (int k = 0; k < 4; ++k) {
-      plan.header[k] = h[k];
-      plan.header_host[k] = h[k];
-    }
-  }
+// Records of key (t, h) in segment j.
+struct KeyRange {
+  const uint32_t* r32;  // non-null: rec32 records
+  const uint16_t* r16;  // else rec16 records
+  uint32_t a, e;
+};
+__device__ __forceinline__ KeyRange seg_key(const Segs& sg, int j, uint32_t F, uint32_t t, uint32_t h) {
+  const MetaLayout L = meta_layout(F);
+  const uint32_t* m = sg.meta[j];
+  const uint32_t k = 2 * t + h;
+  const uint32_t a = m[L.kbase() + k], c = m[L.kcnt() + k];
+  const bool d = (m[L.dbits() + (t >> 5)] >> (t & 31u)) & 1u;
+  return KeyRange{d ? sg.rec32[j] : nullptr, d ? nullptr : sg.rec16[j], a, a + c};
+}
+__device__ __forceinline__ uint32_t seg_key_count(const Segs& sg, int j, uint32_t F, uint32_t k) {
+  return sg.meta[j][meta_layout(F).kcnt() + k];
 }
 
-// The same plan from ceil(F / 1024) workgroups (k_plan's single workgroup walks
-// ~31 strided tiles per thread and is latency-bound): k_plan_a classifies tile
-// t = 1024 b + thread with coalesced reads and stores its workgroup's four item
-// counts in header[4 + k B + b]; k_plan_b scans those, rebuilds each tile's class
-// from tile_tot and writes the lists in tile order (the same order as k_plan).
+// k_plan_a / k_plan_b (ceil(F / 1024) workgroups each): k_plan_a classifies tile
+// t = 1024 b + thread (cold: <= cold_limit records; else big, accumulated per half
+// in chunks of hot_chunk records) and stores its workgroup's item counts in
+// header[4 + k B + b]; k_plan_b scans those and writes the lists in tile order.
 struct PlanCls {
-  uint32_t ci, hi, hot, si, h0;
+  uint32_t ci, hot, si, h0;
 };
-__device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t t, uint32_t tot, int final_mode,
-                                                 uint32_t cold_limit, uint32_t hot_chunk) {
-  PlanCls r{0u, 0u, 0u, 0u, 0xFFFFFFFFu};
+__device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t F, uint32_t t, uint32_t& tot,
+                                                 int final_mode, uint32_t cold_limit, uint32_t hot_chunk) {
+  uint32_t h0 = 0, h1 = 0;
+  for (int j = 0; j < segs.n; ++j) {
+    h0 += seg_key_count(segs, j, F, 2 * t);
+    h1 += seg_key_count(segs, j, F, 2 * t + 1);
+  }
+  tot = h0 + h1;
+  PlanCls r{0u, 0u, 0u, h0};
   if (tot > cold_limit) {
     r.hot = 1;
-    uint32_t h0 = segs.n == 0 ? 0xFFFFFFFFu : 0u;
-    for (int j = 0; j < segs.n; ++j) {
-      const uint16_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
-      if (m == NO_SPLIT) {
-        h0 = 0xFFFFFFFFu;
-        break;
-      }
-      h0 += segs.sinfo[j][SINFO_H0 + m];
-    }
-    r.h0 = h0;
-    if (h0 != 0xFFFFFFFFu)
-      r.si = (h0 + hot_chunk - 1) / hot_chunk + (tot - h0 + hot_chunk - 1) / hot_chunk;
-    else
-      r.hi = (tot + hot_chunk - 1) / hot_chunk;
+    r.si = (h0 + hot_chunk - 1) / hot_chunk + (h1 + hot_chunk - 1) / hot_chunk;
   } else if (final_mode || tot > 0) {
     r.ci = 1;
   }
@@ -136,24 +64,23 @@ __device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t t, u
 
 __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
                                                  uint32_t hot_chunk, Plan plan) {
-  __shared__ uint32_t red[4][17];
+  __shared__ uint32_t red[3][17];
   const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
-  PlanCls c{0u, 0u, 0u, 0u, 0u};
+  PlanCls c{0u, 0u, 0u, 0u};
   if (t < F) {
-    uint32_t tot = 0;
-    for (int j = 0; j < segs.n; ++j) tot += segs.tbase[j][t + 1] - segs.tbase[j][t];
+    uint32_t tot;
+    c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
     plan.tile_tot[t] = tot;
-    c = plan_classify(segs, t, tot, final_mode, cold_limit, hot_chunk);
   }
-  const uint32_t v[4] = {c.ci, c.hot, c.hi, c.si};  // header order
+  const uint32_t v[3] = {c.ci, c.hot, c.si};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 3; ++k) {
     const uint32_t x = wave_sum((uint64_t)v[k]);
     if (lane == 0) red[k][w] = x;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < 3) {
     uint32_t x = 0;
     for (int q = 0; q < 16; ++q) x += red[threadIdx.x][q];
     plan.header[4 + threadIdx.x * gridDim.x + blockIdx.x] = x;
@@ -165,63 +92,57 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   __shared__ uint4 lds4[17];
   __shared__ uint32_t base[4];
   __shared__ uint32_t nbig;
-  __shared__ uint4 big[64];  // {tile | split << 31, first item, half-0 records, records}
+  __shared__ uint4 big[64];  // {tile, first item, half-0 records, records}
   if (threadIdx.x == 0) nbig = 0;  // (visible after the scans' barriers)
   const uint32_t B = gridDim.x;
-  // workgroup bases: the earlier workgroups' counts (B <= 1024: a thread per workgroup),
-  // summed by one reduction; workgroup 0 also writes the header totals
   {
     uint32_t x[4], tx[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
+    for (int k = 0; k < 3; ++k) x[k] = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
+    x[3] = 0u;
     block_excl_scan4<1024>(x, lds4, tx);
     if (threadIdx.x < 4) base[threadIdx.x] = tx[threadIdx.x];
     if (blockIdx.x == 0) {
       uint32_t y[4], ty[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
+      for (int k = 0; k < 3; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
+      y[3] = 0u;
       block_excl_scan4<1024>(y, lds4, ty);
-      if (threadIdx.x < 4) {  // header: cold items, big tiles, mixed-half items, split items
-        plan.header[threadIdx.x] = ty[threadIdx.x];
-        plan.header_host[threadIdx.x] = ty[threadIdx.x];  // read by the host in development builds
+      if (threadIdx.x == 0) {  // header: cold items, big tiles, (unused), split items
+        plan.header[0] = ty[0];
+        plan.header[1] = ty[1];
+        plan.header[2] = 0u;
+        plan.header[3] = ty[2];
       }
     }
   }
   __syncthreads();
   const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
-  PlanCls c{0u, 0u, 0u, 0u, 0xFFFFFFFFu};
+  PlanCls c{0u, 0u, 0u, 0u};
   uint32_t tot = 0;
-  if (t < F) {
-    tot = plan.tile_tot[t];
-    c = plan_classify(segs, t, tot, final_mode, cold_limit, hot_chunk);
-  }
-  uint32_t pv[4] = {c.ci, c.hot, c.hi, c.si}, ptot[4];
+  if (t < F) c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
+  uint32_t pv[4] = {c.ci, c.hot, c.si, 0u}, ptot[4];
   block_excl_scan4<1024>(pv, lds4, ptot);
-  uint32_t ca = base[0] + pv[0];
+  const uint32_t ca = base[0] + pv[0];
   const uint32_t xa = base[1] + pv[1];
-  uint32_t ha = base[2] + pv[2];
-  uint32_t sa = base[3] + pv[3];
+  uint32_t sa = base[2] + pv[2];
   // a tile with many chunk items (C3's tile 0: ~1000) has them written by the whole
   // workgroup below, not by its one thread
   bool coop = false;
-  if (t < F && c.hot && c.si + c.hi > 32) {
+  if (t < F && c.hot && c.si > 32) {
     const uint32_t k = atomicAdd(&nbig, 1u);
     if (k < 64) {
-      big[k] = make_uint4(t | (c.h0 != 0xFFFFFFFFu ? 0x80000000u : 0u), c.h0 != 0xFFFFFFFFu ? sa : ha, c.h0, tot);
+      big[k] = make_uint4(t, sa, c.h0, tot);
       coop = true;
     }
   }
   if (t < F) {
     uint8_t flags = dirty[t] ? TF_DIRTY : 0;
     if (c.hot) {
-      if (c.h0 != 0xFFFFFFFFu) {
-        flags |= TF_SPLIT;
-        for (uint32_t h = 0; !coop && h < 2; ++h) {
-          const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
-          for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
-        }
-      } else if (!coop) {
-        for (uint32_t q = 0; q < c.hi; ++q) plan.hot_item[ha + q] = t | (q << 15);
+      flags |= TF_SPLIT;
+      for (uint32_t h = 0; !coop && h < 2; ++h) {
+        const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
+        for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
       }
       plan.hot_list[xa] = t;
     } else if (c.ci) {
@@ -233,16 +154,10 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   const uint32_t nb = min(nbig, 64u);
   for (uint32_t k = 0; k < nb; ++k) {
     const uint4 e = big[k];
-    const uint32_t tt = e.x & 0x7FFFFFFFu;
-    if (e.x >> 31) {  // split: half 0's chunks, then half 1's
-      const uint32_t n0 = (e.z + hot_chunk - 1) / hot_chunk, n1 = (e.w - e.z + hot_chunk - 1) / hot_chunk;
-      for (uint32_t i = threadIdx.x; i < n0 + n1; i += 1024) {
-        const uint32_t h = i >= n0 ? 1u : 0u;
-        plan.split_item[e.y + i] = make_uint2(tt | (h << 15), h ? i - n0 : i);
-      }
-    } else {
-      const uint32_t n = (e.w + hot_chunk - 1) / hot_chunk;
-      for (uint32_t i = threadIdx.x; i < n; i += 1024) plan.hot_item[e.y + i] = tt | (i << 15);
+    const uint32_t n0 = (e.z + hot_chunk - 1) / hot_chunk, n1 = (e.w - e.z + hot_chunk - 1) / hot_chunk;
+    for (uint32_t i = threadIdx.x; i < n0 + n1; i += 1024) {
+      const uint32_t h = i >= n0 ? 1u : 0u;
+      plan.split_item[e.y + i] = make_uint2(e.x | (h << 15), h ? i - n0 : i);
     }
   }
 }
@@ -262,10 +177,9 @@ __device__ __forceinline__ BigRows big_rows(const State& st, const Outputs& out,
   return BigRows{st.counts + (size_t)t * TILE * ROW, (uint32_t)ROW};
 }
 
-// k_hot_init: split tiles accumulate with global atomics into state rows, so
-// clean ones start from zero.
-// Persistent (the number of hot tiles, header[1], is read on the device).
-__global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, Outputs out, int direct_out, uint32_t hot_chunk) {
+// k_hot_init: big tiles accumulate with global atomics, so clean ones start from
+// zero.  Persistent (the number of big tiles, header[1], is read on the device).
+__global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, Outputs out, int direct_out) {
   const uint32_t nh = plan.header[1];
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const uint32_t t = plan.hot_list[i];
@@ -284,11 +198,6 @@ __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, Outputs o
     if (threadIdx.x < s1 - s0) st.total[s0 + threadIdx.x] = 0;
   }
 }
-
-struct SrcLds32 {  // u32 row in LDS (half-tiles of big tiles), bins 1798/1799 zero
-  const uint32_t* row;
-  __device__ __forceinline__ uint4 get4(int b0) const { return *reinterpret_cast<const uint4*>(row + b0); }
-};
 
 // One series of a tile whose new-record counts sit in LDS (`lds`, u16-packed or
 // u32 row) and whose new samples sum to `vsum` (+ sumfix): merge with the old state if the
@@ -314,7 +223,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
       if (q < NB4) {
         const int b0 = 4 * q;
         const uint4 v = lds.get4(b0);
-        if (orow && !(g_dbg & 0x200)) {
+        if (orow) {
           if (al16 && b0 != 1796)
             *reinterpret_cast<uint4*>(orow + b0) = v;
           else
@@ -347,7 +256,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   if (dirty) total += st.total[s];
   if (lane == 0 && keep) st.total[s] = total;
   if (lane == 0 && emit && out.totals) out.totals[oi] = total;
-  if (emit && !(g_dbg & 0x40000)) {  // 0x40000 (timing): no summaries
+  if (emit) {
     Summary88* so = out.summ ? out.summ + oi : nullptr;
     if (dirty)
       wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
@@ -356,9 +265,9 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   }
 }
 
-// Count a batch of K records per lane (~0u: no record): all bucket-LUT reads are
-// issued before any LDS atomic (the compiler cannot move a read above an atomic
-// it may alias), then per record one histogram atomic and one lane-private sum.
+// Count a batch of K level-1 records per lane (~0u: no record): all bucket-LUT
+// reads are issued before any LDS atomic (the compiler cannot move a read above an
+// atomic it may alias), then per record one histogram atomic and one lane-private sum.
 template <int K, class Hist, class Sum>
 __device__ __forceinline__ void count_batch(const uint32_t (&rec)[K], const uint2* __restrict__ lut2, Hist&& hist_add,
                                             Sum&& sum_add) {
@@ -377,229 +286,113 @@ __device__ __forceinline__ void count_batch(const uint32_t (&rec)[K], const uint
   }
 }
 
-// Records of tile t in the virtual range [vlo, vhi) of its concatenated segments.
-template <int NT = WG, class Fn>
-__device__ __forceinline__ void for_tile_records(const Segs& segs, uint32_t t, uint64_t vlo, uint64_t vhi, Fn&& fn) {
-  uint64_t vbase = 0;
-  for (int j = 0; j < segs.n; ++j) {
-    const uint32_t a = segs.tbase[j][t];
-    const uint32_t e = segs.tbase[j][t + 1];
-    const uint64_t len = e - a;
-    const uint64_t lo = vlo > vbase ? vlo : vbase;
-    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
-    if (lo < hi) {
-      const uint32_t ra = a + (uint32_t)(lo - vbase);
-      for_records<NT>(segs.recs[j], ra, ra + (uint32_t)(hi - lo), fn);
-    }
-    vbase += len;
-  }
-}
-
-// k_accum_cold: one work item = the series of a cold tile (<= cold_limit records)
-// in u16-packed LDS bins, one pass over the tile's records, then one wave per
-// series emits the dense row and the summary.  NSER = 16: the item is one half of
-// the tile, so two 512-thread workgroups of 70 KB share a CU and one's emission
-// overlaps the other's counting; the two halves of a tile are blocks b and b+8,
-// which the round-robin dispatch puts on the same XCD, so the second read of the
-// tile's records mostly hits that XCD's L2 (speed only).  NSER = 32: the whole
-// tile in one 1024-thread workgroup.
-template <int NSER, int NT>
-__global__ __launch_bounds__(NT, 4) void k_accum_cold(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                   uint32_t cold_items, int final_mode, int reset) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t item = blockIdx.x, half = 0;
-  if (NSER == 16) {
-    item = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);
-    half = (blockIdx.x / 8) & 1u;
-  }
-  if (item >= cold_items) return;
-  const uint32_t t = plan.cold_tile[item];
-  const int w = threadIdx.x >> 6;
-  const bool keep = !(final_mode && reset);
-  const uint32_t s0 = t * TILE + half * 16;  // first series of the item
-  uint32_t* hist = smem;                     // [NSER][900] u16 pairs
-  uint32_t* vsl = smem + NSER * CROW;        // [NSER][64] lane-private value sums (< 1152 x 2^21 per slot)
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
-  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [NSER] sumfix of the item's series
-  const int lane = lane_id();
-  // a record of the tile's other half (NSER = 16) counts as no record
-  auto own = [&](uint32_t rec) {
-    return (NSER == 32 || ((rec >> 25) & 1u) == half) ? rec : 0xFFFFFFFFu;
-  };
-  auto hist_add = [&](uint32_t loc, uint32_t b) {
-    atomicAdd(&hist[(loc & (NSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-  };
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & (NSER - 1)) * 64 + lane], v); };
-  // one pending segment (the common case): the tile's first 8 records per lane
-  // are loaded before the LDS is cleared, so their latency overlaps the clearing
-  const bool one = segs.n == 1 && !(g_dbg & 0x100);
-  const uint32_t a = one ? segs.tbase[0][t] : 0u, e = one ? segs.tbase[0][t + 1] : 0u;  // no segment: no read
-  const uint32_t a4 = a & ~3u;
-  auto ld = [&](uint32_t g) {
-    return g < e ? *reinterpret_cast<const uint4*>(segs.recs[0] + g) : make_uint4(0u, 0u, 0u, 0u);
-  };
-  uint32_t g = a4 + 4u * threadIdx.x;
-  uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
-  if (one) {
-    n0 = ld(g);
-    n1 = ld(g + 4u * NT);
-  }
-  if (threadIdx.x < NSER) {  // the item's sumfix entries (read and cleared here)
-    const uint32_t s = s0 + threadIdx.x;
-    int64_t f = 0;
-    if (s < st.S) {
-      f = st.sumfix[s];
-      if (f) st.sumfix[s] = 0;
-    }
-    fixl[threadIdx.x] = f;
-  }
-  {
-    uint4* p = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < (NSER * CROW + NSER * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
-  }
-  __syncthreads();
-  if (one) {
-    for (uint32_t c = a4; c < e; c += 8u * NT, g += 8u * NT) {
-      const uint4 x0 = n0, x1 = n1;
-      n0 = ld(g + 8u * NT);
-      n1 = ld(g + 12u * NT);
-      uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+// Level-2 records of one 16-B group (8 u16; m = valid records): bins only.
+template <class Hist>
+__device__ __forceinline__ void count16(uint4 x, uint32_t m, Hist&& hist_add) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t gk = g + (k >> 2) * 4u * NT + (k & 3);
-        x[k] = (gk < a || gk >= e) ? 0xFFFFFFFFu : own(x[k]);
-      }
-      count_batch<8>(x, lut2, hist_add, sum_add);
-    }
-  } else if (!(g_dbg & 0x100)) {
-    for_tile_records<NT>(segs, t, 0, plan.tile_tot[t], [&](uint32_t rec) {
-      const uint32_t x[1] = {own(rec)};
-      count_batch<1>(x, lut2, hist_add, sum_add);
-    });
+  for (int k = 0; k < 8; ++k) {
+    if ((uint32_t)k >= m) continue;
+    const uint32_t r = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+    hist_add(r >> 11, r & 2047u);
   }
-  __syncthreads();
-  const bool dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;  // as of k_plan: both halves see the same
-  for (int loc = w; loc < NSER; loc += NT / 64) {
-    const uint32_t s = s0 + loc;
-    if (s >= st.S) continue;
-    const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
-    emit_series(SrcLds16{hist + loc * CROW}, s, vsum, fixl[loc], dirty, keep, final_mode, st, tb, out);
-  }
-  if (threadIdx.x == 0 && half == 0) st.dirty[t] = keep ? 1 : 0;
 }
 
-// k_accum_cold_p: the persistent form of k_accum_cold.  NSER = 32: one 1024-thread
-// workgroup per CU walks the cold items blockIdx.x, + gridDim.x, ...; NSER = 16:
-// two 512-thread workgroups per CU, one half-tile each.  The LUT is
-// staged once, each wave clears its series' LDS rows right after emitting them
-// (no clearing phase), and the next item's record range, first 8 records per
-// lane, sumfix entries and dirty flag are loaded before the current item's
-// emission, so their latency hides behind it (and behind its dense stores).
-template <int NSER, int NT>
-__global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                      uint32_t cold_arg, int final_mode, int reset) {
+// The records of both halves of tile t in every segment: per segment, the two
+// ranges are walked together (a thread's loads of both halves in flight at once).
+// Ranges start 16-B aligned (rec32 regions at multiples of 4, rec16 of 8).
+template <int NT, class Hist, class Sum>
+__device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t t, const uint2* __restrict__ lut2,
+                                           Hist&& hist_add, Sum&& sum_add) {
+  for (int j = 0; j < sg.n; ++j) {
+    const KeyRange r0 = seg_key(sg, j, F, t, 0), r1 = seg_key(sg, j, F, t, 1);
+    if (r0.r32) {
+      const uint32_t n0 = r0.e - r0.a, n1 = r1.e - r1.a;
+      const uint32_t g0 = (n0 + 3) / 4, g1 = (n1 + 3) / 4, gm = max(g0, g1);
+      const uint4* p0 = reinterpret_cast<const uint4*>(r0.r32 + r0.a);
+      const uint4* p1 = reinterpret_cast<const uint4*>(r1.r32 + r1.a);
+      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+        const uint4 x = g < g0 ? p0[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        const uint4 y = g < g1 ? p1[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (4 * g + k >= n0) v[k] = 0xFFFFFFFFu;
+          if (4 * g + k >= n1) v[4 + k] = 0xFFFFFFFFu;
+        }
+        count_batch<8>(v, lut2, hist_add, sum_add);
+      }
+    } else {
+      const uint32_t n0 = r0.e - r0.a, n1 = r1.e - r1.a;
+      const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
+      const uint4* p0 = reinterpret_cast<const uint4*>(r0.r16 + r0.a);
+      const uint4* p1 = reinterpret_cast<const uint4*>(r1.r16 + r1.a);
+      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+        const uint4 x = g < g0 ? p0[g] : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 y = g < g1 ? p1[g] : make_uint4(0u, 0u, 0u, 0u);
+        count16(x, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
+        count16(y, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
+      }
+    }
+  }
+}
+
+// k_accum_cold_p: one 1024-thread workgroup per CU walks the cold tiles (<= 65535
+// records: u16 bins cannot overflow) blockIdx.x, + gridDim.x, ...: 32 series in
+// u16-packed LDS bins, lane-private u32 value sums of the level-1 records, then one
+// wave per series emits the dense row and the summary.  The LUT and the midpoints
+// are staged once; each wave clears its series' LDS rows right after emitting them.
+__global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                                          uint32_t cold_arg, int final_mode, int reset) {
+  constexpr int NT = 1024;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t cold_items = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
-  uint32_t* hist = smem;                                      // [NSER][900] u16 pairs
-  uint32_t* vsl = smem + NSER * CROW;                         // [NSER][64] lane-private value sums
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + NSER * 64);    // [LUT2_N]
-  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [NSER] sumfix of the item's series
-  int32_t* midl = reinterpret_cast<int32_t*>(fixl + NSER);     // [NB] bucket midpoints (the summary's lookups)
+  uint32_t* hist = smem;                                      // [32][900] u16 pairs
+  uint32_t* vsl = smem + TILE * CROW;                         // [32][64] lane-private value sums
+  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);    // [LUT2_N]
+  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the item's series
+  int32_t* midl = reinterpret_cast<int32_t*>(fixl + TILE);    // [NB] bucket midpoints (the summary's lookups)
   const int w = threadIdx.x >> 6;
   const int lane = lane_id();
   const bool keep = !(final_mode && reset);
-  const bool one = segs.n == 1 && !(g_dbg & 0x100);
-  const uint32_t* __restrict__ r0 = segs.recs[0];
+  const uint32_t F = st.F;
   Tables tbl = tb;
   tbl.mid = midl;
-  // NSER = 16: blocks b and b + 8 (same XCD under the round-robin dispatch) walk the
-  // same tiles, one half each, so a tile's records are read from HBM about once
-  uint32_t first = blockIdx.x, stride = gridDim.x, half = 0;
-  if (NSER == 16) {
-    first = (blockIdx.x / 16) * 8 + (blockIdx.x % 8);
-    half = (blockIdx.x / 8) & 1u;
-    stride = gridDim.x / 2;
-  }
-  // a record of the tile's other half counts as no record
-  auto own = [&](uint32_t rec) { return (NSER == 32 || ((rec >> 25) & 1u) == half) ? rec : 0xFFFFFFFFu; };
   auto hist_add = [&](uint32_t loc, uint32_t b) {
-    atomicAdd(&hist[(loc & (NSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+    atomicAdd(&hist[(loc & 31u) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
   };
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & (NSER - 1)) * 64 + lane], v); };
-  auto ld = [&](uint32_t g, uint32_t e) {
-    return g < e ? *reinterpret_cast<const uint4*>(r0 + g) : make_uint4(0u, 0u, 0u, 0u);
-  };
+  // (a slot gathers <= 65535 / 64 records of one lane of ONE wave per tile: < 2^32)
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 31u) * 64 + lane], v); };
   {
     uint4* p = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < (NSER * CROW + NSER * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
     for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
   }
-  // the next item: tile, record range, first records, sumfix entry, dirty flag
-  uint32_t item = first;
-  uint32_t t = 0, a = 0, e = 0;
-  uint4 n0 = make_uint4(0u, 0u, 0u, 0u), n1 = n0;
-  int64_t f = 0;
-  bool dirty = false;
-  auto fetch = [&](uint32_t it) {
-    if (it >= cold_items) return;
-    t = plan.cold_tile[it];
-    dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;
-    if (one) {
-      a = segs.tbase[0][t];
-      e = segs.tbase[0][t + 1];
-      const uint32_t g = (a & ~3u) + 4u * threadIdx.x;
-      n0 = ld(g, e);
-      n1 = ld(g + 4u * NT, e);
-    }
-    if (threadIdx.x < NSER) {
-      const uint32_t s = t * TILE + half * 16 + threadIdx.x;
-      f = 0;
+  __syncthreads();
+  for (uint32_t item = blockIdx.x; item < cold_items; item += gridDim.x) {
+    const uint32_t t = plan.cold_tile[item];
+    const bool dc = (plan.tile_flags[t] & TF_DIRTY) != 0;
+    if (threadIdx.x < TILE) {  // the tile's sumfix entries (read and cleared here)
+      const uint32_t s = t * TILE + threadIdx.x;
+      int64_t f = 0;
       if (s < st.S) {
         f = st.sumfix[s];
         if (f) st.sumfix[s] = 0;
       }
+      fixl[threadIdx.x] = f;
     }
-  };
-  fetch(item);
-  __syncthreads();
-  for (; item < cold_items; item += stride) {
-    const uint32_t tc = t;
-    const bool dc = dirty;
-    if (threadIdx.x < NSER) fixl[threadIdx.x] = f;
-    if (one) {
-      const uint32_t a4 = a & ~3u;
-      uint32_t g = a4 + 4u * threadIdx.x;
-      for (uint32_t c = a4; c < e; c += 8u * NT, g += 8u * NT) {
-        const uint4 x0 = n0, x1 = n1;
-        n0 = ld(g + 8u * NT, e);
-        n1 = ld(g + 12u * NT, e);
-        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t gk = g + (k >> 2) * 4u * NT + (k & 3);
-          x[k] = (gk < a || gk >= e) ? 0xFFFFFFFFu : own(x[k]);
-        }
-        count_batch<8>(x, lut2, hist_add, sum_add);
-      }
-    } else if (!(g_dbg & 0x100)) {
-      for_tile_records<NT>(segs, tc, 0, plan.tile_tot[tc], [&](uint32_t rec) {
-        const uint32_t x[1] = {own(rec)};
-        count_batch<1>(x, lut2, hist_add, sum_add);
-      });
-    }
+    count_tile<NT>(segs, F, t, lut2, hist_add, sum_add);
     __syncthreads();  // counts complete; fixl visible
-    fetch(item + stride);
-    const uint32_t s0 = tc * TILE + half * 16;
+    const uint32_t s0 = t * TILE;
     // linear emission: a clean whole tile inside the output range of a resetting
     // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
     // of 14384 16-B chunks by the whole workgroup in step -- 5.6 TB/s against 4.1 for
     // per-wave rows (tools/mb_store.hip) -- after the per-series summaries
     const uint32_t oi0 = s0 - out.first;
-    const bool linear = NSER == 32 && !keep && !dc && out.counts != nullptr && s0 >= out.first &&
-                        oi0 + TILE <= out.count && s0 + TILE <= st.S && (oi0 & 1u) == 0u && !(g_dbg & 0x4000000);
-    for (int loc = w; loc < NSER; loc += NT / 64) {
+    const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
+                        s0 + TILE <= st.S && (oi0 & 1u) == 0u;
+    for (int loc = w; loc < TILE; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
@@ -609,8 +402,7 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
           uint32_t g[9];
 #pragma unroll
           for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(SrcLds16{row}.get4(28 * lane + 4 * q)) : 0u;
-          if (!(g_dbg & 0x40000))
-            wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
           if (lane == 0 && out.totals) out.totals[s - out.first] = (int64_t)vsum + fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
@@ -635,123 +427,24 @@ __global__ __launch_bounds__(NT, 1) void k_accum_cold_p(Segs segs, Plan plan, St
         // the second pair is the next word (one ds_read2/ds_write2), except for the
         // chunk that straddles into the next row (b0 = 1796)
         uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
-        uint32_t x, y;
-        if (b0 != NB - 2) {
-          x = p0[0];
-          y = p0[1];
-          p0[0] = 0u;
-          p0[1] = 0u;
-        } else {
-          x = *p0;
-          y = *p1;
-          *p0 = 0u;
-          *p1 = 0u;
-        }
-        if (!(g_dbg & 0x200)) o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+        const uint32_t x = *p0, y = *p1;
+        *p0 = 0u;
+        *p1 = 0u;
+        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
       }
     }
-    if (threadIdx.x == 0 && half == 0) st.dirty[tc] = keep ? 1 : 0;
+    if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
     __syncthreads();  // rows cleared, fixl consumed
-  }
-}
-
-// Big tiles (> cold_limit records) not split in every pending segment: item = (tile,
-// chunk of <= hot_chunk records of its concatenated segments), the whole tile's 32
-// series in u16-packed LDS bins (115 KB, like a cold tile), each record read once.
-// A bin that reaches 2^15 hands 2^15 to the state row (one global atomic; the half
-// never reaches 2^16, so it cannot carry into its neighbour); at the end every
-// nonzero bin is flushed with global atomics into the rows k_hot_init cleared, and
-// k_hot_finish summarizes them.  Lane-private u64 value sums.
-__global__ __launch_bounds__(WG) void k_accum_hot(Segs segs, Plan plan, State st, Tables tb, Outputs out, int direct_out,
-                                                  uint32_t hot_chunk) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* hist = smem;                                                                // [32][CROW] u16 pairs
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + TILE * CROW);  // [32][64]
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);                              // [LUT2_N]
-  const int lane = lane_id();
-  const int w = threadIdx.x >> 6;
-  const uint32_t nitems = plan.header[2];  // persistent: items blockIdx.x, + gridDim.x, ...
-  for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
-  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-    {
-      uint4* q = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    const uint32_t hx = plan.hot_item[item];
-    const uint32_t t = hx & 0x7FFFu;
-    const uint64_t vlo = (uint64_t)(hx >> 15) * hot_chunk, vhi = vlo + hot_chunk;
-    const BigRows br = big_rows(st, out, plan, t, direct_out);
-    uint32_t* tile_rows = br.base;
-    auto hist_add = [&](uint32_t loc, uint32_t b) {
-      if (g_dbg & 0x2000) return;
-      const uint32_t sh = (b & 1u) * 16u;
-      uint32_t* wd = &hist[(loc & 31u) * CROW + (b >> 1)];
-      const uint32_t old = atomicAdd(wd, 1u << sh);
-      if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {  // this add made it 2^15: hand 2^15 over
-        atomicSub(wd, 0x8000u << sh);
-        atomicAdd(&tile_rows[(size_t)(loc & 31u) * br.stride + b], 0x8000u);
-      }
-    };
-    auto sum_add = [&](uint32_t loc, uint32_t v) {
-      if (!(g_dbg & 0x4000)) atomicAdd(&vsl[(loc & 31u) * 64 + lane], (unsigned long long)v);
-    };
-    uint64_t vbase = 0;
-    for (int j = 0; j < segs.n; ++j) {
-      const uint32_t ta = segs.tbase[j][t], te = segs.tbase[j][t + 1];
-      const uint64_t len = te - ta;
-      const uint64_t lo = vlo > vbase ? vlo : vbase;
-      const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
-      const uint64_t skip = lo - vbase;
-      vbase += len;
-      if (lo >= hi) continue;
-      const uint32_t a = ta + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
-      const uint32_t* __restrict__ r = segs.recs[j];
-      auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
-      const uint32_t a4 = a & ~3u;
-      uint32_t g = a4 + 4u * threadIdx.x;
-      uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
-      for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
-        const uint4 x0 = n0, x1 = n1;
-        n0 = ld(g + 8u * WG);
-        n1 = ld(g + 12u * WG);
-        uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
-          if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
-        }
-        count_batch<8>(x, lut2, hist_add, sum_add);
-      }
-    }
-    __syncthreads();
-    for (int loc = w; loc < TILE; loc += WG / 64) {
-      const uint32_t s = t * TILE + loc;
-      if (s >= st.S) continue;
-      const uint64_t vsum = wave_sum(vsl[loc * 64 + lane]);
-      uint32_t* grow = tile_rows + (size_t)loc * br.stride;
-      const uint32_t* hrow = hist + loc * CROW;
-      for (int b0 = 0; b0 < ((g_dbg & 0x1000) ? 0 : NB); b0 += 64) {  // 64 consecutive bins per wave atomic
-        const int b = b0 + lane;
-        const uint32_t v = b < NB ? (hrow[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu : 0u;
-        if (__ballot(v != 0u)) {
-          if (v) atomicAdd(&grow[b], v);
-        }
-      }
-      if (lane == 0 && vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)vsum);
-    }
-    __syncthreads();  // the LDS rows are read: the next item may clear them
   }
 }
 
 // One-tile series spaces (S <= 32: C1, the head shard of a many-way C3) fold each
 // batch into the tile's state rows at ingest -- no records, no partition, no
 // segment.  k_fold1_init clears the rows of a clean tile and marks it dirty;
-// k_fold1 items are chunks of the batch, counted like k_accum_hot's (u16-packed
-// LDS bins of the 32 series, a 2^15 hand-off to the state row, nonzero bins flushed
+// k_fold1 items are chunks of the batch: u16-packed LDS bins of the 32 series with a
+// 2^15 hand-off to the state row (or u32 bins for <= 16 series), nonzero bins flushed
 // with global atomics, lane-private u64 value sums into total; escapes go to sumfix
-// as at ingest).  Invalid ids are dropped and reported like k_count's.  W32: at most
-// 16 series (C1), u32 LDS bins (non-returning atomics, no hand-off).
+// as at ingest.  Invalid ids are dropped and counted.
 __global__ __launch_bounds__(256) void k_fold1_init(State st) {
   const bool clean = st.dirty[0] == 0;
   if (clean) {
@@ -873,121 +566,145 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
   if (bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
 }
 
-// Split big tiles (split in every pending segment): item = (tile, half, chunk of
-// hot_chunk records of that half).  A segment holds the tile's half-0 records at
-// [tbase, tbase + h0) and its half-1 records after them, so each item reads one
-// contiguous range per segment, with no filtering.  u32 LDS bins for the half's
-// 16 series, lane-private value sums, flushed with global atomics (k_hot_init
-// cleared the rows; k_hot_finish summarizes them).
+// Big tiles: item = (tile, half, chunk of hot_chunk records of that half across the
+// pending segments; each segment holds the half as one contiguous range).  u32 LDS
+// bins for the half's 16 series, lane-private u64 value sums of the level-1 records,
+// flushed with global atomics (k_hot_init cleared the rows; k_hot_finish
+// summarizes them).
 __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                     int direct_out, uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t nitems = plan.header[3];  // persistent: items blockIdx.x, + gridDim.x, ...
-  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-  const uint2 it = plan.split_item[item];
-  const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
+  const uint32_t F = st.F;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   uint32_t* hist = smem;                                                              // [16][1800]
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64] u64, as in k_accum_hot
-  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);  // [LUT2_N]
-  {
-    uint4* q = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
-  }
-  __syncthreads();
-  const uint64_t vlo = (uint64_t)it.y * hot_chunk, vhi = vlo + hot_chunk;
-  uint64_t vbase = 0;
-  for (int j = 0; j < segs.n; ++j) {
-    const uint32_t m = reinterpret_cast<const uint16_t*>(segs.sinfo[j] + SINFO_MAP)[t];
-    const uint32_t h0 = segs.sinfo[j][SINFO_H0 + m];
-    const uint32_t ta = segs.tbase[j][t], te = segs.tbase[j][t + 1];
-    const uint32_t a0 = half ? ta + h0 : ta;
-    const uint64_t len = half ? te - ta - h0 : h0;
-    const uint64_t lo = vlo > vbase ? vlo : vbase;
-    const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
-    const uint64_t skip = lo - vbase;
-    vbase += len;
-    if (lo >= hi) continue;
-    const uint32_t a = a0 + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
-    const uint32_t* __restrict__ r = segs.recs[j];
-    auto ld = [&](uint32_t g) { return g < e ? *reinterpret_cast<const uint4*>(r + g) : make_uint4(0u, 0u, 0u, 0u); };
-    const uint32_t a4 = a & ~3u;
-    uint32_t g = a4 + 4u * threadIdx.x;
-    uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
-    for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
-      const uint4 x0 = n0, x1 = n1;
-      n0 = ld(g + 8u * WG);
-      n1 = ld(g + 12u * WG);
-      uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64]
+  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);             // [LUT2_N]
+  for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
+  auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); };
+  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); };
+  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const uint2 it = plan.split_item[item];
+    const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
+    {
+      uint4* q = reinterpret_cast<uint4*>(smem);
+      for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    const uint64_t vlo = (uint64_t)it.y * hot_chunk, vhi = vlo + hot_chunk;
+    uint64_t vbase = 0;
+    for (int j = 0; j < segs.n; ++j) {
+      const KeyRange r = seg_key(segs, j, F, t, half);
+      const uint64_t len = r.e - r.a;
+      const uint64_t lo = vlo > vbase ? vlo : vbase;
+      const uint64_t hi = vhi < vbase + len ? vhi : vbase + len;
+      const uint64_t skip = lo - vbase;
+      vbase += len;
+      if (lo >= hi) continue;
+      // [a, e) of this range; hot_chunk is a multiple of 1024, so a chunk starts 16-B aligned
+      const uint32_t a = r.a + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
+      if (r.r32) {
+        const uint32_t a4 = a & ~3u;
+        auto ld = [&](uint32_t g) {
+          return g < e ? *reinterpret_cast<const uint4*>(r.r32 + g) : make_uint4(0u, 0u, 0u, 0u);
+        };
+        uint32_t g = a4 + 4u * threadIdx.x;
+        uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
+        for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
+          const uint4 x0 = n0, x1 = n1;
+          n0 = ld(g + 8u * WG);
+          n1 = ld(g + 12u * WG);
+          uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
-        if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+            if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
+          }
+          count_batch<8>(x, lut2, hist_add, sum_add);
+        }
+      } else {
+        const uint32_t a8 = a & ~7u;
+        auto ld = [&](uint32_t g) {
+          return g < e ? *reinterpret_cast<const uint4*>(r.r16 + g) : make_uint4(0u, 0u, 0u, 0u);
+        };
+        uint32_t g = a8 + 8u * threadIdx.x;
+        uint4 n0 = ld(g), n1 = ld(g + 8u * WG);
+        for (uint32_t c = a8; c < e; c += 16u * WG, g += 16u * WG) {
+          const uint4 x0 = n0, x1 = n1;
+          n0 = ld(g + 16u * WG);
+          n1 = ld(g + 24u * WG);
+          const uint4 xs[2] = {x0, x1};
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const uint32_t wd[4] = {xs[q].x, xs[q].y, xs[q].z, xs[q].w};
+            const uint32_t gq = g + (uint32_t)q * 8u * WG;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t gk = gq + (uint32_t)k;
+              if (gk < a || gk >= e) continue;
+              const uint32_t rr = (wd[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+              hist_add(rr >> 11, rr & 2047u);
+            }
+          }
+        }
       }
-      count_batch<8>(
-          x, lut2, [&](uint32_t loc, uint32_t b) { if (!(L5DH_EXP & 2)) atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); },
-          [&](uint32_t loc, uint32_t v) {
-            if (!(L5DH_EXP & 1)) atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v);
-          });
     }
-  }
-  __syncthreads();
-  const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
-  const uint32_t s = t * TILE + 16 * half + w;
-  if (s < st.S) {
-    const BigRows br = big_rows(st, out, plan, t, direct_out);
-    uint32_t* grow = br.base + (size_t)(16 * half + w) * br.stride;
-    const uint32_t* hrow = hist + w * HROW;
-    for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
-      const int b = b0 + lane;
-      const uint32_t v = b < NB ? hrow[b] : 0u;
-      if (__ballot(v != 0u)) {
-        if (v) atomicAdd(&grow[b], v);
+    __syncthreads();
+    const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
+    const uint32_t s = t * TILE + 16 * half + w;
+    if (s < st.S) {
+      const BigRows br = big_rows(st, out, plan, t, direct_out);
+      uint32_t* grow = br.base + (size_t)(16 * half + w) * br.stride;
+      const uint32_t* hrow = hist + w * HROW;
+      for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+        const int b = b0 + lane;
+        const uint32_t v = b < NB ? hrow[b] : 0u;
+        if (__ballot(v != 0u)) {
+          if (v) atomicAdd(&grow[b], v);
+        }
       }
+      if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
     }
-    if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
-  }
-  __syncthreads();  // the LDS rows are read: the next item may clear them
+    __syncthreads();  // the LDS rows are read: the next item may clear them
   }
 }
 
-// k_hot_finish: per (hot tile, half): fold sumfix, summarize the merged rows,
+// k_hot_finish: per (big tile, half): fold sumfix, summarize the merged rows,
 // write outputs, update state/dirty.
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
-                                                   int reset, int direct_out, uint32_t hot_chunk) {
-  const uint32_t nv = 2 * plan.header[1];  // persistent: (hot tile, half) pairs
+                                                   int reset, int direct_out) {
+  const uint32_t nv = 2 * plan.header[1];  // persistent: (big tile, half) pairs
   for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
-  const uint32_t t = plan.hot_list[vb >> 1];
-  const uint32_t half = vb & 1u;
-  const int lane = lane_id();
-  const int w = threadIdx.x >> 6;
-  const uint32_t s = t * TILE + 16 * half + w;
-  if (s < st.S) {
-    int64_t total = st.total[s] + st.sumfix[s];
-    if (final_mode) {
-      const uint32_t oi = s - out.first;
-      if (s >= out.first && oi < out.count) {
-        uint32_t g[9];
-        if (direct_out && !(plan.tile_flags[t] & TF_DIRTY)) {  // counted in the output row itself
-          const SrcExt src{out.counts + (size_t)oi * NB};
-          row_pass(src, g, nullptr);
-          wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
-        } else {
-          const SrcRow32 src{st.counts + (size_t)s * ROW};
-          row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
-          wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+    const uint32_t t = plan.hot_list[vb >> 1];
+    const uint32_t half = vb & 1u;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t s = t * TILE + 16 * half + w;
+    if (s < st.S) {
+      int64_t total = st.total[s] + st.sumfix[s];
+      if (final_mode) {
+        const uint32_t oi = s - out.first;
+        if (s >= out.first && oi < out.count) {
+          uint32_t g[9];
+          if (direct_out && !(plan.tile_flags[t] & TF_DIRTY)) {  // counted in the output row itself
+            const SrcExt src{out.counts + (size_t)oi * NB};
+            row_pass(src, g, nullptr);
+            wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+          } else {
+            const SrcRow32 src{st.counts + (size_t)s * ROW};
+            row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
+            wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+          }
+          if (lane == 0 && out.totals) out.totals[oi] = total;
         }
-        if (lane == 0 && out.totals) out.totals[oi] = total;
+      }
+      if (lane == 0) {
+        st.sumfix[s] = 0;
+        st.total[s] = total;
       }
     }
-    if (lane == 0) {
-      st.sumfix[s] = 0;
-      st.total[s] = total;
-    }
-  }
-  if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
+    if (threadIdx.x == 0 && half == 0) st.dirty[t] = (final_mode && reset) ? 0 : 1;
   }
 }
 
@@ -1040,50 +757,7 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
   }
 }
 
-}  // namespace
-
-hipError_t set_snapshot_debug(int dbg) {
-  g_dbg_host = dbg;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dbg, sizeof(int));
-}
-
-hipError_t set_snapshot_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)acc_cold_lds(32));
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold_p<32, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)acc_cold_p_lds(32));
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold_p<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)acc_cold_p_lds(16));
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold<16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)acc_cold_lds(16));
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
-}
-
-hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
-                       const uint8_t* dirty, Plan plan, hipStream_t st) {
-  // single-workgroup plan past 2^20 tiles (k_plan_b scans <= 1024 workgroup counts),
-  // or with L5DH_DBG bit 0x1000000
-  if ((g_dbg_host & 0x1000000) || F > (1u << 20)) {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
-    return hipGetLastError();
-  }
-  const uint32_t B = (F + 1023) / 1024;  // header holds 4 + 4 B words (l5dh_engine.cpp)
-  hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
-  hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
-  return hipGetLastError();
-}
-
-static int num_cus() {
+int num_cus() {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1094,53 +768,47 @@ static int num_cus() {
   return ncu;
 }
 
-hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, uint32_t hot_chunk,
-                           hipStream_t st) {
-  if (max_hot == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hot_init, dim3(std::min<uint32_t>(max_hot, 4u * num_cus())), dim3(256), 0, st, plan, state,
-                     out, direct_out, hot_chunk);
+}  // namespace
+
+hipError_t set_snapshot_attributes() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)acc_cold_p_lds(32));
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
+}
+
+hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
+                       const uint8_t* dirty, Plan plan, hipStream_t st) {
+  const uint32_t B = (F + 1023) / 1024;  // header holds 4 + 3 B words (l5dh_engine.cpp)
+  hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
+  hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
   return hipGetLastError();
 }
 
-hipError_t launch_accum(Segs segs, Plan plan, uint32_t cold_items, uint32_t max_hot_items, State state, Tables tb,
-                        Outputs out, uint32_t cold_limit, uint32_t hot_chunk, int final_mode, int reset,
-                        int direct_out, hipStream_t st) {
-  const uint32_t ncu = (uint32_t)num_cus();
-  if (cold_items) {
-    // default: the persistent form, one 1024-thread workgroup per CU walking the cold
-    // tiles (-3 % against a workgroup per tile, measured); cold_items may be DEV_COUNT
-    // (read on the device).  Development builds (L5DH_DBG, host counts only): bit
-    // 0x800000 a workgroup per tile, with 0x20000 half-tile items; bit 0x2000000 the
-    // persistent half-tile form (all measured slower)
-    if (!(g_dbg_host & 0x800000)) {
-      if (g_dbg_host & 0x2000000) {
-        const uint32_t pairs = std::min<uint32_t>(cold_items, ncu);
-        hipLaunchKernelGGL((k_accum_cold_p<16, 512>), dim3(((pairs + 7) / 8) * 16), dim3(512), acc_cold_p_lds(16), st,
-                           segs, plan, state, tb, out, cold_items, final_mode, reset);
-      } else {
-        const uint32_t grid = std::min<uint32_t>(cold_items, ncu);
-        hipLaunchKernelGGL((k_accum_cold_p<32, 1024>), dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan,
-                           state, tb, out, cold_items, final_mode, reset);
-      }
-    } else if (!(g_dbg_host & 0x20000))
-      hipLaunchKernelGGL((k_accum_cold<32, 1024>), dim3(cold_items), dim3(1024), acc_cold_lds(32), st, segs, plan,
-                         state, tb, out, cold_items, final_mode, reset);
-    else
-      hipLaunchKernelGGL((k_accum_cold<16, 512>), dim3(((cold_items + 7) / 8) * 16), dim3(512), acc_cold_lds(16), st,
-                         segs, plan, state, tb, out, cold_items, final_mode, reset);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  if (max_hot_items) {  // persistent: one workgroup per CU walking the chunk items
-    hipLaunchKernelGGL(k_accum_hot, dim3(std::min<uint32_t>(max_hot_items, ncu)), dim3(WG), ACC_HOT_LDS, st, segs,
-                       plan, state, tb, out, direct_out, hot_chunk);
-    return hipGetLastError();
-  }
-  return hipSuccess;
+hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, hipStream_t st) {
+  if (max_hot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hot_init, dim3(std::min<uint32_t>(max_hot, 4u * num_cus())), dim3(256), 0, st, plan, state,
+                     out, direct_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
+                             int final_mode, int reset, hipStream_t st) {
+  if (cold_items == 0) return hipSuccess;
+  // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
+  // may be DEV_COUNT (read on the device)
+  const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
+  hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan, state, tb, out,
+                     cold_items, final_mode, reset);
+  return hipGetLastError();
 }
 
 hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, uint32_t chunk, State state, Tables tb,
-                       uint32_t* err, bool vec, bool wide, hipStream_t st) {
+                        uint32_t* err, bool vec, bool wide, hipStream_t st) {
   hipLaunchKernelGGL(k_fold1_init, dim3(1), dim3(256), 0, st, state);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1164,10 +832,10 @@ hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, St
 }
 
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
-                             int reset, int direct_out, uint32_t hot_chunk, hipStream_t st) {
+                             int reset, int direct_out, hipStream_t st) {
   if (max_hot == 0) return hipSuccess;
   hipLaunchKernelGGL(k_hot_finish, dim3(std::min<uint32_t>(2 * max_hot, 2u * num_cus())), dim3(WG), 0, st, plan, state,
-                     tb, out, final_mode, reset, direct_out, hot_chunk);
+                     tb, out, final_mode, reset, direct_out);
   return hipGetLastError();
 }
 

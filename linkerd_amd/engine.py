@@ -268,6 +268,13 @@ class HistogramEngine:
                     "l5dh_merge")
         return (first.value, count.value, out[:count.value]) if own else (first.value, count.value)
 
+    def merge_bytes(self) -> dict:
+        """l5dh_merge_bytes: dense / encoded / sent bytes of the last merge."""
+        d, e, s = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._check(self._lib.l5dh_merge_bytes(self._ctx, ctypes.byref(d), ctypes.byref(e), ctypes.byref(s)),
+                    "l5dh_merge_bytes")
+        return {"dense": d.value, "encoded": e.value, "sent": s.value}
+
     # -- plumbing -------------------------------------------------------------
     def sync(self):
         self._check(self._lib.l5dh_sync(self._ctx), "l5dh_sync")

@@ -9,7 +9,9 @@
   (l5dh_export_state), a reduce-scatter sums them (integer sums: bit-exact and
   order independent) so rank r owns series slice r, which it summarizes with
   l5dh_summarize_dense.  min/max are midpoints derived from counts, so they need
-  no separate min/max reduction.
+  no separate min/max reduction.  The library's own exchange (l5dh_merge) moves the
+  rows sparse: sparse_encode / sparse_decode below restate its format, and
+  fleet_merge(mode="sparse") runs the same exchange over torch.distributed.
 """
 from __future__ import annotations
 
@@ -143,3 +145,95 @@ def fleet_merge(counts, totals, group=None, mode: str = "reduce_scatter", S: Opt
     first = rank * per
     keep = max(0, min(per, S - first))
     return c_out[:keep], t_out[:keep], first
+
+
+# ---- the sparse row exchange of l5dh_merge (linkerd_amd/csrc/l5dh_merge.hip) ----
+CMAX = 0x1FFFFF  # count field of an entry; CMAX marks a count in the next word
+
+
+def sparse_encode(rows: np.ndarray):
+    """Rows int32 [n][1798] -> (entries u32, words per row u32): per row its non-empty
+    buckets in bucket order, bucket << 21 | count, or bucket << 21 | CMAX followed by
+    the count's 32 bits when count >= CMAX (the encoding k_menc writes)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int32).view(np.uint32)
+    r, b = np.nonzero(rows)
+    c = rows[r, b]
+    esc = c >= CMAX
+    head = (b.astype(np.uint32) << 21) | np.where(esc, CMAX, c).astype(np.uint32)
+    enc = np.empty(head.size + int(esc.sum()), np.uint32)
+    pos = np.arange(head.size) + np.concatenate([[0], np.cumsum(esc)[:-1]]).astype(np.int64) if head.size else \
+        np.zeros(0, np.int64)
+    enc[pos] = head
+    enc[pos[esc] + 1] = c[esc]
+    words = np.bincount(r, minlength=rows.shape[0]).astype(np.uint32) + \
+        np.bincount(r[esc], minlength=rows.shape[0]).astype(np.uint32)
+    return enc, words
+
+
+def sparse_decode(sources, nrows: int) -> np.ndarray:
+    """Sum of the rows encoded by several ranks: sources = [(entries, words per row)]
+    of the same nrows rows (k_mdecode's arithmetic, one row at a time)."""
+    out = np.zeros((nrows, NB), np.int64)
+    for enc, words in sources:
+        offs = np.concatenate([[0], np.cumsum(words.astype(np.int64))])
+        for r in range(nrows):
+            i, e = int(offs[r]), int(offs[r + 1])
+            while i < e:
+                x = int(enc[i])
+                c = x & CMAX
+                if c == CMAX:
+                    c = int(enc[i + 1])
+                    i += 1
+                out[r, x >> 21] += c
+                i += 1
+    return out.astype(np.int32)
+
+
+def sparse_reduce_scatter(counts, totals, group=None, S: Optional[int] = None):
+    """l5dh_merge's reduce-scatter over torch.distributed (gloo tests): rank q sends
+    each rank r the sparse encoding of r's row slice and the words per row (an
+    all-gather of the slice sizes first, as the library sizes its receive buffers),
+    the totals are summed densely.  Returns (counts_slice, totals_slice, first,
+    bytes_sent)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    S = counts.shape[0] if S is None else int(S)
+    Sp = padded_rows(S, world)
+    per = Sp // world
+    rows = np.zeros((Sp, NB), np.int32)
+    rows[:S] = counts[:S].cpu().numpy()
+    parts = [sparse_encode(rows[q * per:(q + 1) * per]) for q in range(world)]
+    sizes = torch.tensor([p[0].size for p in parts], dtype=torch.int64)
+    mat = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(mat, sizes, group=group)
+    sent = 0
+    recv = [None] * world
+    reqs = []
+    for q in range(world):
+        if q == rank:
+            recv[q] = parts[q]
+            continue
+        enc, words = parts[q]
+        sent += 4 * enc.size + 4 * per + 8 * per
+        reqs.append(dist.isend(torch.from_numpy(enc.view(np.int32).copy()), q, group=group))
+        reqs.append(dist.isend(torch.from_numpy(words.view(np.int32).copy()), q, group=group))
+    for q in range(world):
+        if q == rank:
+            continue
+        e = torch.empty(int(mat[q][rank]), dtype=torch.int32)
+        w = torch.empty(per, dtype=torch.int32)
+        dist.recv(e, q, group=group)
+        dist.recv(w, q, group=group)
+        recv[q] = (e.numpy().view(np.uint32), w.numpy().view(np.uint32))
+    for rq in reqs:
+        rq.wait()
+    c_out = torch.from_numpy(sparse_decode(recv, per))
+    tt = torch.zeros(Sp, dtype=torch.int64)
+    tt[:S] = totals[:S].cpu()
+    dist.all_reduce(tt, op=dist.ReduceOp.SUM, group=group)
+    first = rank * per
+    keep = max(0, min(per, S - first))
+    return c_out[:keep], tt[first:first + per][:keep].clone(), first, sent

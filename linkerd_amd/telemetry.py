@@ -123,8 +123,8 @@ class StatEngine:
 
     def _flush_locked(self, st: "_Staging") -> None:
         if st.n:
-            self.engine.ingest(st.ids[: st.n], st.vals[: st.n])
-            st.n = 0
+            n, st.n = st.n, 0  # cleared first: a failed call is never re-sent (no double count)
+            self.engine.ingest(st.ids[:n], st.vals[:n])
 
     def flush(self) -> None:
         with self._lock:
@@ -199,6 +199,10 @@ class Metric:
 
         def __init__(self, engine: Optional[StatEngine] = None):
             self._engine = engine
+            # the per-Stat monitor of Metric.scala:30-33: add() reads the id and stages
+            # its sample under it, and _release() takes the id away under it, so once
+            # _release has run no add can stage the old id (which may be re-issued)
+            self._lock = threading.Lock()
             self.series_id = engine.register() if engine is not None else None
             self._summary_snapshot: Optional[HistogramSummary] = None
             self._reset_time = time.time()
@@ -214,9 +218,11 @@ class Metric:
             return self._reset_time
 
         def add(self, value: float) -> None:
-            if self.series_id is None and self._engine is not None:
-                return  # pruned: like adding to a histogram no exporter reads any more
-            self._eng().add(self.series_id, value)
+            with self._lock:
+                sid = self.series_id  # read once
+                if sid is None and self._engine is not None:
+                    return  # pruned: like adding to a histogram no exporter reads any more
+                self._eng().add(sid, value)
 
         def peek(self) -> List[BucketAndCount]:
             if self.series_id is None and self._engine is not None:
@@ -224,8 +230,12 @@ class Metric:
             return self._eng().peek(self.series_id)
 
         def _release(self) -> None:
-            """MetricsTree.prune: hand the series id back to the engine."""
-            sid, self.series_id = self.series_id, None
+            """MetricsTree.prune: hand the series id back to the engine.  The id is
+            taken under the Stat's lock, so every add that saw it has already staged its
+            sample; StatEngine.release then flushes those and clears the row before the
+            id is handed out again."""
+            with self._lock:
+                sid, self.series_id = self.series_id, None
             if self._engine is not None and sid is not None:
                 self._engine.release(sid)
 

@@ -57,13 +57,14 @@ def test_header_constants_match_host():
 
     assert define("L5DH_NLIMITS") == N.NLIMITS == 1797
     assert define("L5DH_NBUCKETS") == N.NBUCKETS == 1798
-    assert define("L5DH_ABI_VERSION") == 2
+    assert define("L5DH_ABI_VERSION") == 3
     enum = dict((k, int(v)) for k, v in re.findall(r"(L5DH_(?:PARAM|K)_[A-Z0-9_]+) = (\d+)", h))
     assert enum["L5DH_PARAM_TIMING"] == N.PARAM_TIMING
     assert enum["L5DH_PARAM_COLD_LIMIT"] == N.PARAM_COLD_LIMIT
     assert enum["L5DH_PARAM_HOT_CHUNK"] == N.PARAM_HOT_CHUNK
     assert enum["L5DH_PARAM_MAX_SEGMENTS"] == N.PARAM_MAX_SEGMENTS
-    assert enum["L5DH_PARAM_BIN_MODE"] == N.PARAM_BIN_MODE
+    assert enum["L5DH_PARAM_REGION_PCT"] == N.PARAM_REGION_PCT
+    assert "L5DH_PARAM_BIN_MODE" not in enum and "L5DH_PARAM_SPLIT_MIN" not in enum  # removed in ABI 3
     assert [enum[f"L5DH_K_{n}"] for n in ("COUNT", "SCAN", "BIN", "ACCUM", "HOT", "COPY", "BIN2")] == \
         [N.K_COUNT, N.K_SCAN, N.K_BIN, N.K_ACCUM, N.K_HOT, N.K_COPY, N.K_BIN2]
     assert enum["L5DH_K_NKERNELS"] == len(N.KERNEL_NAMES)
@@ -73,7 +74,7 @@ def test_header_constants_match_host():
 
 
 def test_abi_version_and_limits(lib, oracle):
-    assert lib.l5dh_abi_version() == 2
+    assert lib.l5dh_abi_version() == 3
     lim = N.limits()
     assert lim.dtype == np.int32 and lim.shape == (N.NLIMITS,)
     np.testing.assert_array_equal(lim, oracle.limits())

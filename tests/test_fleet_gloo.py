@@ -34,6 +34,12 @@ def _worker(rank, world, port, S, N, mode, out_dir, padded=False):
     h.ingest(series[mine], vals[mine])
     counts = torch.from_numpy(h.counts())
     totals = torch.from_numpy(h.totals())
+    if mode == "sparse":  # l5dh_merge's exchange: sparse slices over send/recv, dense totals
+        c, t, first, sent = fleet.sparse_reduce_scatter(counts, totals)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), counts=c.numpy(), totals=t.numpy(), first=first, sent=sent)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if padded:  # alloc_dense buffers: merged without a padded copy
         cb, tb = fleet.alloc_dense(S, world)
         cb[:S] = counts
@@ -47,8 +53,10 @@ def _worker(rank, world, port, S, N, mode, out_dir, padded=False):
 
 
 @pytest.mark.parametrize("padded", [False, True], ids=["copy", "alloc_dense"])
-@pytest.mark.parametrize("mode", ["reduce_scatter", "all_reduce"])
+@pytest.mark.parametrize("mode", ["reduce_scatter", "all_reduce", "sparse"])
 def test_fleet_merge_gloo_bitexact(tmp_path, mode, padded):
+    if mode == "sparse" and padded:
+        pytest.skip("the sparse exchange pads internally")
     S, N, world = 301, 60_000, 2  # S not divisible by world: padded reduce-scatter
     mp.start_processes(_worker, args=(world, _free_port(), S, N, mode, str(tmp_path), padded), nprocs=world,
                        start_method="spawn")
@@ -69,6 +77,10 @@ def test_fleet_merge_gloo_bitexact(tmp_path, mode, padded):
     np.testing.assert_array_equal(got_t, want_t)
     # the merged rows summarize exactly like the single-process histograms
     assert O.summarize_counts(got_c, got_t).tobytes() == h.snapshot().tobytes()
+    if mode == "sparse":  # what went over the wire: well under the dense rows' (W-1)/W
+        dense = (S + 1) // 2 * (fleet.NB * 4 + 8)
+        sent = [int(np.load(tmp_path / f"r{r}.npz")["sent"]) for r in range(world)]
+        assert all(0 < b < dense // 4 for b in sent), (sent, dense)
 
 
 def test_shard_ranges_balanced_and_router():

@@ -54,7 +54,7 @@ def test_export_reset_fused_matches_oracle(oracle, dev_bufs):
     eng.ingest(*batches[0])
     o.ingest(*batches[0])
     eng.snapshot(reset=False)  # folds into state: dirty tiles
-    for b in batches[1:]:      # two pending segments, the second with a split set
+    for b in batches[1:]:      # two pending segments, the second sized from the first
         eng.ingest(*b)
         o.ingest(*b)
     if dev_bufs:

@@ -67,6 +67,39 @@ def test_merge_one_rank_matches_oracle(oracle, form, mode, rccl):
     eng.close()
 
 
+@pytest.mark.parametrize("value", [7.0, 3e9], ids=["bucket", "overflow"])
+def test_merge_sparse_escaped_counts(oracle, value):
+    """The sparse exchange's escape: one bucket of one series holds 2.5M > 2^21 - 1
+    samples, so its count takes a second word; the decoder must take that word as a
+    count (whatever its low bits) -- through RCCL at one rank, against the oracle."""
+    from linkerd_amd.engine import HistogramEngine
+    S = 300
+    rng = np.random.default_rng(7)
+    hot = np.zeros(2_500_000, np.uint32)
+    cold = rng.integers(0, S, 200_000).astype(np.uint32)
+    series = np.concatenate([hot, cold])
+    vals = np.concatenate([np.full(hot.size, value, np.float32),
+                           np.exp(2 + rng.standard_normal(cold.size)).astype(np.float32)])
+    perm = rng.permutation(series.size)
+    series, vals = series[perm], vals[perm]
+    eng = HistogramEngine(S)
+    eng.set_param(N.PARAM_MERGE_RCCL_1RANK, 1)
+    eng.comm_init_rank(HistogramEngine.comm_unique_id(), 1, 0)
+    eng.ingest(series, vals)
+    counts = np.zeros((S, N.NBUCKETS), np.int32)
+    totals = np.zeros(S, np.int64)
+    first, count, summ = eng.merge(N.MERGE_REDUCE_SCATTER, counts=counts, totals=totals)
+    o = oracle.OracleHistograms(S)
+    o.ingest(series, vals)
+    np.testing.assert_array_equal(counts, o.counts())
+    np.testing.assert_array_equal(totals, o.totals())
+    _eq_summaries(summ, o.snapshot())
+    mb = eng.merge_bytes()
+    assert mb["dense"] == S * (N.NBUCKETS * 4 + 8) and 0 < mb["encoded"] < mb["dense"]
+    eng.comm_destroy()
+    eng.close()
+
+
 def test_merge_without_communicator_is_einval():
     from linkerd_amd.engine import HistogramEngine
     eng = HistogramEngine(64)
@@ -226,8 +259,8 @@ def _stream_ordered_body(oracle, torch, HistogramEngine):
     eng.close()
 
 
-@pytest.mark.parametrize("mode", [2, 3], ids=["twolevel", "paged"])
-def test_snapshot_stream_ordered_on_caller_stream(oracle, mode):
+@pytest.mark.parametrize("pct", [100, 40], ids=["regions", "redo"])
+def test_snapshot_stream_ordered_on_caller_stream(oracle, pct):
     """An engine on torch's stream (l5dh_set_stream) with device outputs returns from
     l5dh_snapshot without a host wait: batches generated, ingested and snapshotted
     back to back, each snapshot read by torch work queued behind it, no synchronize
@@ -238,7 +271,7 @@ def test_snapshot_stream_ordered_on_caller_stream(oracle, mode):
     dev = torch.device("cuda", 0)
     with torch.cuda.stream(torch.cuda.Stream()):
         eng = HistogramEngine(S)
-        eng.set_param(N.PARAM_BIN_MODE, mode)
+        eng.set_param(N.PARAM_REGION_PCT, pct)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         batches = [synth.c3(S=S, N=400_000, seed=90 + k) for k in range(4)]
         dbat = [(torch.from_numpy(sr.astype(np.int32)).to(dev), torch.from_numpy(v).to(dev)) for sr, v in batches]

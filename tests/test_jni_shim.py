@@ -1,7 +1,8 @@
 """The JVM side of the boundary, on CPU: the JNI shim (jni/src/main/native/l5dh_jni.c)
 must keep compiling against include/l5dhist.h (checked with a declarations-only
 JNI stub, tests/jni_stub/jni.h: this image has no JDK), and the C caller of the ABI
-(tests/c/abi_test.c, built by build()) links and runs without a GPU."""
+(tests/c/abi_test.c) and the fake-JNIEnv driver of the shim (tests/c/jni_fake_env.c,
+run on the GPU by tests/test_gpu_jni.py) link and start without a GPU."""
 import os
 import re
 import shutil
@@ -33,4 +34,14 @@ def test_c_caller_links_the_library():
     if not os.path.exists(exe):
         pytest.skip("not built (run build())")
     r = subprocess.run([exe, "--version"], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0 and r.stdout.strip() == "2"
+    assert r.returncode == 0 and r.stdout.strip() == "3"
+
+
+def test_fake_jnienv_driver_links_the_shim():
+    """tests/c/jni_fake_env.c (built by build()): the shim and the library link into one
+    program; without arguments it prints its usage and touches no device."""
+    exe = os.path.join(REPO, "linkerd_amd", "lib", "l5dh_jni_fake_env")
+    if not os.path.exists(exe):
+        pytest.skip("not built (run build())")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
