@@ -11,8 +11,8 @@ the previous batch) is tested on a batch it has not seen.
 Workloads (synthetic inputs generated on the GPU):
   c3 (default)  1M series, 1e9 samples per step in total, Zipf(s=1) series ids,
                 log-normal values.  With N ranks the series space is split into
-                contiguous ranges of equal expected device time (a per-sample +
-                per-series cost model over the Zipf pmf, fleet.shard_ranges) and
+                contiguous ranges of equal modelled device time (fleet.plan_shards:
+                a per-sample + per-series cost model over the per-tile load) and
                 each rank ingests the samples of its range: series-sharded, no
                 collective, strong scaling.
   c4            fleet merge: the same 1M series, the 1e9 samples sample-sharded
@@ -57,23 +57,12 @@ KERNEL_ALG_BYTES = {
     "accum": lambda n, s, fleet: (7192 if fleet else 7280) * s,  # writes counts (+ summary)
 }
 METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
-# device cost model of one step on MI355X, for the C3 shard plan: a base model
-# (COST_PS_PER_SAMPLE per Zipf-expected sample + COST_PS_PER_SERIES per series row)
-# times a measured correction per Zipf-rank range -- each range's measured shard
-# time over its base-model time, from the 8 single-GPU runs of `--shard r/8`
-# (the sweep profiles/r02q_shards_before.jsonl, after the stream-ordered snapshot): direct
-# tiles, split tiles through level 2 and cold tiles cost differently per sample
-COST_PS_PER_SAMPLE = 6.5
-ONE_TILE = 32  # series of one tile: such a series space is folded at ingest (k_fold1)
-# the first tile as one shard, folded at ingest (ms, `--shard 0/8` of the pinned plan); the
-# calibration's first entry prices it partitioned (1.28 ms measured for its first 15 series)
-COST_FIRST_TILE_FOLDED = 0.8274
-COST_PS_PER_SERIES = 1700.0
-COST_CALIBRATION = ((0, 1.5), (32, 1.0543), (438, 1.0466), (4084, 1.0721), (22645, 1.0502), (99791, 1.034),
-                    (300417, 1.0519), (615688, 1.0599))  # (first Zipf rank, ms of that r/8 shard)
-# the same from the 4- and 2-way sweeps (a plan of W ranks uses the sweep of W, else the 8-way one)
-COST_CALIBRATION_W = {4: ((0, 2.2185), (190, 2.1285), (15832, 2.0186), (272830, 2.0488)),
-                      2: ((0, 4.1812), (15832, 3.8621))}
+# device cost model of one step on MI355X for the C3 shard plan (fleet.CostModel): one
+# per-sample, per-series and fold cost for any series / sample count, fitted to the
+# measured single-GPU steps; the plan is derived from per-tile loads
+# (fleet.plan_shards) -- here the workload's expected load, in a fleet the previous
+# interval's l5dh_tile_totals
+C3_COST = dict(per_sample=5.5e-9, per_series=2.0e-6, per_sample_fold=3.0e-9, fixed=0.05)
 
 
 def parse():
@@ -133,9 +122,8 @@ def plan(args, world: int, rank: int) -> dict:
             base = rank * (N // world) + min(rank, N % world)
             return dict(workload=wl, S_total=S, N_total=N, first=0, count=S, samples=n, base_index=base,
                         world=world, rank=rank, scaling="strong")
-        # balanced by expected device time: COST_PS_PER_SAMPLE per Zipf-expected
-        # sample + COST_PS_PER_SERIES per series row (balancing by samples alone
-        # would leave the last rank most of the dense series rows)
+        # balanced by modelled device time over the per-tile load (balancing by samples
+        # alone would leave the last rank most of the dense series rows)
         shards = shard_plan(S, N, world, cdf)
         sh = shards[rank]
         mass = [float(cdf[x.first + x.count - 1] - (cdf[x.first - 1] if x.first else 0.0)) if x.count else 0.0
@@ -154,39 +142,22 @@ def plan(args, world: int, rank: int) -> dict:
                 base_index=0, world=world, rank=rank, scaling="weak")
 
 
-def shard_plan(S, N, world, cdf):
-    """C3 series ranges of equal expected device time.  A one-tile head shard is
-    folded at ingest (k_fold1, about half the device time per sample of a
-    partitioned shard, but only while it holds <= ONE_TILE series): the plan pins
-    rank 0 to the first tile when that lowers the expected slowest rank, else it
-    balances every rank over the partitioned costs."""
-    from linkerd_amd import fleet
-    w = shard_cost(cdf, N, world)  # partitioned costs, the first tile included
-    plain = fleet.shard_ranges(S, world, weights=w)
-    if world == 1 or S <= ONE_TILE:
-        return plain
-    cost = lambda x: float(w[x.first:x.first + x.count].sum())
-    calibrated = S == S_C3 and N == N_C3
-    folded = COST_FIRST_TILE_FOLDED if calibrated else 0.5 * float(w[:ONE_TILE].sum())
-    rest = fleet.shard_ranges(S - ONE_TILE, world - 1, weights=w[ONE_TILE:])
-    pinned = [fleet.Shard(0, 0, ONE_TILE)] + [fleet.Shard(x.rank + 1, x.first + ONE_TILE, x.count) for x in rest]
-    if max([folded] + [cost(x) for x in pinned[1:]]) < max(cost(x) for x in plain):
-        return pinned
-    return plain
-
-
-def shard_cost(cdf, N, world=8):
-    """Expected device time per series of the C3 workload (COST_* above)."""
+def expected_tile_load(cdf, N):
+    """Samples per 32-series tile the Zipf workload puts on each tile (its expected
+    load: what l5dh_tile_totals reports for a batch, up to sampling noise)."""
     import numpy as np
     S = cdf.size
-    pmf = np.diff(np.concatenate([[0.0], cdf]))
-    w = COST_PS_PER_SAMPLE * N * pmf + COST_PS_PER_SERIES
-    if S == S_C3 and N == N_C3:  # the calibration is of this workload
-        cal = COST_CALIBRATION_W.get(world, COST_CALIBRATION)
-        edges = [a for a, _ in cal] + [S]
-        for (a, ms), b in zip(cal, edges[1:]):
-            w[a:b] *= ms / w[a:b].sum()
-    return w
+    c = np.concatenate([[0.0], cdf])
+    edges = np.minimum(np.arange(0, S + 32, 32), S)
+    edges = np.unique(edges)
+    return N * np.diff(c[edges])
+
+
+def shard_plan(S, N, world, cdf):
+    """C3 series ranges of equal modelled device time (fleet.plan_shards over the
+    expected per-tile load, fleet.CostModel C3_COST)."""
+    from linkerd_amd import fleet
+    return fleet.plan_shards(expected_tile_load(cdf, N), S, world, fleet.CostModel(**C3_COST))
 
 
 def gen_batch(torch, synth_lib, pl, seed_off, stream):

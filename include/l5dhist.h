@@ -206,6 +206,11 @@ int l5dh_merge(l5dh_ctx* ctx, int mode, l5dh_summary* out, int32_t* counts_out, 
 int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_t** counts_outs,
                    int64_t** totals_outs, uint32_t* firsts, uint32_t* counts);
 
+/* Records per 32-series tile of the last binned ingest batch (out: >= ceil(max_series
+ * / 32) entries; staged samples are binned first).  The load a series-sharded fleet
+ * plans its next ranges from (linkerd_amd/fleet.py plan_shards). */
+int l5dh_tile_totals(l5dh_ctx* ctx, uint64_t* out, size_t n);
+
 /* Bytes of the last l5dh_merge / l5dh_merge_all on this context (any pointer nullable):
  * *dense = the dense rows + totals a reduce-scatter would move ([S][1798] int32 +
  * [S] int64), *encoded = this rank's sparse encoding of them (non-empty buckets,

@@ -198,6 +198,7 @@ struct l5dh_ctx {
   uint32_t direct_max = DIRECT_MAX;  // direct tiles per batch (0: none)
   uint32_t direct_div = 1;           // direct tiles average >= 1/direct_div records per 8K samples
   uint32_t region_pct = 100;         // region capacity scale (L5DH_PARAM_REGION_PCT)
+  uint64_t fold_last = 0;            // samples of the last batch folded at ingest (one-tile spaces)
   DevBuf stage_series, stage_values, stage_summ, stage_counts, stage_totals, stage_in_counts, stage_in_totals;
   // staging ring: small ingest batches are concatenated on the device and binned together
   DevBuf ring_series, ring_values;
@@ -466,6 +467,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     const uint32_t chunk =
         (uint32_t)std::min<size_t>(c->hot_chunk & ~3u, std::max<size_t>(16384, (fill + 1023) & ~(size_t)1023));
     HIPCHK(c, launch_fold1(ds, dv, n, chunk, state(c), tables(c), c->d_err, vec, (c->variant & 1) != 0, c->stream));
+    c->fold_last = n;
     HIPCHK(c, hipMemcpyAsync(c->h_header + 4, c->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     return 0;
   }
@@ -1432,6 +1434,24 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
                           counts ? counts + i : nullptr)))
       return r;
   }
+  return 0;
+}
+
+int l5dh_tile_totals(l5dh_ctx* c, uint64_t* out, size_t n) {
+  if (!c || !out) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (n < c->F) return fail(c, -EINVAL, "tile totals: the output holds fewer than ceil(max_series / 32) entries");
+  hipSetDevice(c->device);
+  int r;
+  if ((r = flush_ring(c))) return r;
+  if (c->F == 1) {  // folded at ingest: the batch's samples (invalid ids included)
+    out[0] = c->fold_last;
+    return sync_stream(c);
+  }
+  std::vector<uint32_t> k(2 * (size_t)c->F);
+  HIPCHK(c, hipMemcpyAsync(k.data(), c->d_kprev, k.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  if ((r = sync_stream(c))) return r;
+  for (uint32_t t = 0; t < c->F; ++t) out[t] = (uint64_t)k[2 * t] + k[2 * t + 1];
   return 0;
 }
 

@@ -13,11 +13,11 @@
 //   k_rfix1    a run that did not fit its region -> exact regions from the cursors
 //              and a second k_rbin1 pass (launched always, it exits unless needed);
 //              the direct keys' ranges; the invalid-id count to the host
-//   k_rplan2   level-2 regions of the other keys; level-2 items (16K records of a
+//   k_rplan2a/b level-2 regions of the other keys; level-2 items (16K records of a
 //              super-tile's level-1 region)
 //   k_rbin2    level 2: an item LDS-sorted by key into 16-bit records (series in
 //              tile | bucket) in its keys' regions; value sums folded into sumfix
-//   k_rfix2    exact key counts -> kprev (the next batch's prediction); overflow ->
+//   k_rfix2a/b exact key counts -> kprev (the next batch's prediction); overflow ->
 //              exact regions and a second k_rbin2 pass
 //
 // Level-1 record (rec32): [31:26] tile in super-tile | [25:21] series in tile |
@@ -203,13 +203,9 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   }
   __syncthreads();
   uint64_t total;
-  uint64_t base = block_excl_scan64((uint64_t)capl[j], l64, &total);
-  if (total + 16 > cap32) {  // too big for the buffer: scale down (an overflow is redone exactly)
-    const double f = (double)(cap32 - 16) / (double)total;
-    const uint32_t c2 = (uint32_t)((double)capl[j] * f) & ~3u;
-    base = block_excl_scan64((uint64_t)c2, l64, &total);
-    capl[j] = c2;
-  }
+  const uint64_t base = block_excl_scan64((uint64_t)capl[j], l64, &total);
+  if (base + capl[j] + 16 > cap32)  // past the buffer's end: clamped (its runs overflow; level 1 is redone exactly)
+    capl[j] = base + 16 < cap32 ? (uint32_t)(cap32 - 16 - base) & ~3u : 0u;
   meta[L.bbase() + j] = (uint32_t)base;
   meta[L.bcap() + j] = j < TB ? capl[j] : 0u;
   meta[L.bcnt() + j] = 0u;
@@ -498,51 +494,77 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------------
-// Level-2 plan, one workgroup: thread j owns the 64 keys of tiles [32 j, 32 j + 32)
-// and super-tile j's items.
-__global__ __launch_bounds__(1024) void k_rplan2(size_t n, uint32_t F, uint32_t* __restrict__ kest,
-                                                 const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
-                                                 size_t cap16, uint32_t pct) {
+// Level-2 plan over ceil(2F / 1024) workgroups, key k = 1024 b + thread (coalesced):
+// k_rplan2a sizes the regions of the non-direct keys and sums them per workgroup;
+// k_rplan2b adds the earlier workgroups' sums, scans, and clamps a region that would
+// pass the buffer's end (its runs overflow and level 2 is redone exactly); its
+// workgroup 0 also plans the level-2 items (16K records of a super-tile's region).
+__device__ __forceinline__ bool tile_direct(const uint32_t* __restrict__ meta, const MetaLayout& L, uint32_t t) {
+  return (meta[L.dbits() + (t >> 5)] >> (t & 31u)) & 1u;
+}
+
+// The sum of the u64 per-workgroup partials before workgroup b (b <= 64).
+__device__ __forceinline__ uint64_t wsum_before(const uint64_t* __restrict__ ws, uint32_t b, uint64_t* red /*[16]*/) {
+  uint64_t v = threadIdx.x < b ? ws[threadIdx.x] : 0ull;
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t r = 0;
+  for (int q = 0; q < 16; ++q) r += red[q];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(1024) void k_rplan2a(size_t n, uint32_t F, uint32_t* __restrict__ kest,
+                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
+                                                  uint32_t pct) {
+  __shared__ uint64_t red[16];
+  const MetaLayout L = meta_layout(F);
+  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
+  const bool exact = m == n;
+  const double s = m ? (double)n / (double)m : 1.0;
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  uint32_t cap = 0;
+  if (k < L.K) {
+    const uint32_t e = kest[k];
+    if (e) kest[k] = 0;  // ready for the next batch
+    if (!tile_direct(meta, L, k >> 1)) {
+      cap = rcap((double)kprev[k], (double)e, s, exact, 32.0, 8, pct);
+      meta[L.kcap() + k] = cap;
+    }
+  }
+  const uint64_t w = wave_sum((uint64_t)cap);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int q = 0; q < 16; ++q) t += red[q];
+    reinterpret_cast<uint64_t*>(meta + L.wsum())[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restrict__ meta, size_t cap16) {
+  __shared__ uint64_t red[16];
   __shared__ uint64_t l64[17];
   __shared__ uint32_t lds[17];
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
-  const bool exact = m == n;
-  const double s = m ? (double)n / (double)m : 1.0;
-  const uint32_t j = threadIdx.x, t0 = j * 32;
-  const uint32_t dbits = t0 < F ? meta[L.dbits() + j] : 0u;
-  auto key_cap = [&](uint32_t k) -> uint32_t {  // this thread's key 2 t0 + k (0 for direct tiles)
-    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
-    if (t >= F || ((dbits >> (k >> 1)) & 1u)) return 0u;
-    return rcap((double)kprev[key], (double)kest[key], s, exact, 32.0, 8, pct);
-  };
-  uint64_t sum = 0;
-  for (uint32_t k = 0; k < 64; ++k) sum += key_cap(k);
+  const uint64_t before = wsum_before(reinterpret_cast<const uint64_t*>(meta + L.wsum()), blockIdx.x, red);
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
+  uint32_t cap = mine ? meta[L.kcap() + k] : 0u;
   uint64_t total;
-  uint64_t base = block_excl_scan64(sum, l64, &total);
-  double f = 1.0;
-  if (total + 64 > cap16) {  // too big for the buffer: scale down (an overflow is redone exactly)
-    f = (double)(cap16 - 64) / (double)total;
-    sum = 0;
-    for (uint32_t k = 0; k < 64; ++k) sum += (uint32_t)((double)key_cap(k) * f) & ~7u;
-    base = block_excl_scan64(sum, l64, &total);
+  const uint64_t base = before + block_excl_scan64((uint64_t)cap, l64, &total);
+  if (mine) {
+    if (base + cap + 64 > cap16) cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
+    meta[L.kbase() + k] = (uint32_t)base;
+    meta[L.kcap() + k] = cap;
+    meta[L.kcnt() + k] = 0u;
   }
-  for (uint32_t k = 0; k < 64; ++k) {
-    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
-    if (t >= F) break;
-    uint32_t c = key_cap(k);
-    if (f != 1.0) c = (uint32_t)((double)c * f) & ~7u;
-    if (!((dbits >> (k >> 1)) & 1u)) {
-      meta[L.kbase() + key] = (uint32_t)base;
-      meta[L.kcap() + key] = c;
-      meta[L.kcnt() + key] = 0u;
-    }
-    if (kest[key]) kest[key] = 0;  // ready for the next batch
-    base += c;
-  }
-  // level-2 items of super-tile j
+  if (blockIdx.x != 0) return;  // (workgroup-uniform)
+  // level-2 items of super-tile j = thread
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t j = threadIdx.x;
   const uint32_t tot = j < FS ? meta[L.btot() + j] : 0u;
   const uint32_t ni = (tot + ITEM2 - 1) / ITEM2;
   uint32_t all;
@@ -569,18 +591,20 @@ __global__ __launch_bounds__(1024) void k_rplan2(size_t n, uint32_t F, uint32_t*
 // global atomic per non-empty key on its cursor, stage {rec16 | key << 16}, written
 // in order to run base + position.
 constexpr int B2_KEYS = 2 * ST_TILES;
-constexpr size_t rbin2_lds() { return (size_t)ITEM2 * 4 + 2048 * 8 + LUT2_N * 8 + B2_KEYS * 12 + 16; }
+constexpr int B2_NT = 512;  // two workgroups per CU: one's loads and atomics overlap the other's LDS phases
+constexpr size_t rbin2_lds() { return (size_t)ITEM2 * 3 + 2048 * 8 + LUT2_N * 8 + B2_KEYS * 12 + 16; }
 
 template <int NT>
-__global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
+__global__ __launch_bounds__(NT, 4) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
                                                  const uint32_t* __restrict__ rec32, uint16_t* __restrict__ rec16,
                                                  int64_t* __restrict__ sumfix, int pass) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* stage = smem;                                                             // [ITEM2]
-  unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem + ITEM2);     // [2048]
+  unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem);             // [2048]
   uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                                // [LUT2_N]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);                         // [B2_KEYS]
   uint2* ocx = reinterpret_cast<uint2*>(cnt + B2_KEYS);                               // [B2_KEYS]
+  uint16_t* stage = reinterpret_cast<uint16_t*>(ocx + B2_KEYS);                       // [ITEM2] rec16, sorted
+  uint8_t* stagek = reinterpret_cast<uint8_t*>(stage + ITEM2);                        // [ITEM2] their keys
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO2]) == 0u) return;
@@ -674,7 +698,11 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t kr = decode(g, k, xs[k], false);
-        if (kr != NOKEY) stage[ocx[kr >> 16].x + rank[4 * g + k]] = kr;
+        if (kr != NOKEY) {
+          const uint32_t pos = ocx[kr >> 16].x + rank[4 * g + k];
+          stage[pos] = (uint16_t)(kr & 0xFFFFu);
+          stagek[pos] = (uint8_t)(kr >> 16);
+        }
       }
     }
     if (wv < 2) {
@@ -692,9 +720,8 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
     for (int k = 0; k < 4 * PG; ++k) {  // each wave a contiguous range of the stage
       const uint32_t i = (uint32_t)wv * (4 * PG * 64) + (uint32_t)k * 64 + (uint32_t)lane;
       if (i < total) {
-        const uint32_t v = stage[i];
-        const uint2 o = ocx[v >> 16];
-        if (o.y != INVALID) rec16[o.y + (i - o.x)] = (uint16_t)(v & 0xFFFFu);
+        const uint2 o = ocx[stagek[i]];
+        if (o.y != INVALID) rec16[o.y + (i - o.x)] = stage[i];
       }
     }
   }
@@ -702,44 +729,52 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
   if (pass == 0) flush(cur_j);
 }
 
-// After level 2 (one workgroup; thread j owns the 64 keys of tiles [32 j, 32 j + 32)):
-// the exact key counts become the next batch's prediction; on an overflow, exact
-// regions for the redo pass.
-__global__ __launch_bounds__(1024) void k_rfix2(uint32_t F, uint32_t* __restrict__ meta, uint32_t* __restrict__ kprev) {
+// After level 2, over the key workgroups: k_rfix2a copies the exact key counts to
+// kprev (the next batch's prediction; a cursor counts on past an overflow, so they
+// are exact either way), sums their 8-rounded sizes per workgroup and passes the
+// overflow flag on as the redo flag; on a redo, k_rfix2b lays the regions out exactly.
+__global__ __launch_bounds__(1024) void k_rfix2a(uint32_t F, uint32_t* __restrict__ meta, uint32_t* __restrict__ kprev) {
+  __shared__ uint64_t red[16];
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  uint32_t r8 = 0;
+  if (k < L.K) {
+    const uint32_t c = meta[L.kcnt() + k];
+    kprev[k] = c;
+    if (!tile_direct(meta, L, k >> 1)) r8 = round_up(c, 8);
+  }
+  const uint64_t w = wave_sum((uint64_t)r8);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int q = 0; q < 16; ++q) t += red[q];
+    reinterpret_cast<uint64_t*>(meta + L.wsum())[blockIdx.x] = t;
+    if (blockIdx.x == 0) hdr[H_REDO2] = hdr[H_OV2];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_rfix2b(uint32_t F, uint32_t* __restrict__ meta) {
+  __shared__ uint64_t red[16];
   __shared__ uint64_t l64[17];
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
-  const uint32_t ov = hdr[H_OV2];
-  const uint32_t j = threadIdx.x, t0 = j * 32;
-  const uint32_t dbits = t0 < F ? meta[L.dbits() + j] : 0u;
-  uint64_t sum = 0;
-  for (uint32_t k = 0; k < 64; ++k) {
-    const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
-    if (t >= F) break;
-    const uint32_t x = meta[L.kcnt() + key];
-    kprev[key] = x;
-    if (!((dbits >> (k >> 1)) & 1u)) sum += round_up(x, 8);
+  if (hdr[H_REDO2] == 0u) return;  // (grid-uniform)
+  const uint64_t before = wsum_before(reinterpret_cast<const uint64_t*>(meta + L.wsum()), blockIdx.x, red);
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
+  const uint32_t c8 = mine ? round_up(meta[L.kcnt() + k], 8) : 0u;
+  uint64_t total;
+  const uint64_t base = before + block_excl_scan64((uint64_t)c8, l64, &total);
+  if (mine) {
+    meta[L.kbase() + k] = (uint32_t)base;
+    meta[L.kcap() + k] = c8;
+    meta[L.kcnt() + k] = 0u;
   }
-  if (ov) {  // (block-uniform)
-    uint64_t total;
-    uint64_t base = block_excl_scan64(sum, l64, &total);
-    for (uint32_t k = 0; k < 64; ++k) {
-      const uint32_t t = t0 + (k >> 1), key = 2 * t0 + k;
-      if (t >= F) break;
-      if (!((dbits >> (k >> 1)) & 1u)) {
-        const uint32_t c8 = round_up(meta[L.kcnt() + key], 8);
-        meta[L.kbase() + key] = (uint32_t)base;
-        meta[L.kcap() + key] = c8;
-        meta[L.kcnt() + key] = 0u;
-        base += c8;
-      }
-    }
-  }
-  __syncthreads();
-  if (j == 0) {
-    hdr[H_REDO2] = ov;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     hdr[H_OV2] = 0u;
-    if (ov) hdr[H_NOVR2] += 1u;
+    hdr[H_NOVR2] += 1u;
   }
 }
 
@@ -775,7 +810,7 @@ hipError_t set_ingest_attributes() {
   if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rbin1_lds(CH1))))
     return e;
-  return hipFuncSetAttribute((const void*)k_rbin2<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
+  return hipFuncSetAttribute((const void*)k_rbin2<B2_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
 }
 
 hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
@@ -794,16 +829,24 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
         if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);
       }
       break;
-    case 2:  // level-2 plan
-      hipLaunchKernelGGL(k_rplan2, dim3(1), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap16, a.pct);
+    case 2: {  // level-2 plan
+      const uint32_t B = (K + 1023) / 1024;  // <= 64 (wsum)
+      hipLaunchKernelGGL(k_rplan2a, dim3(B), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.pct);
+      hipLaunchKernelGGL(k_rplan2b, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.cap16);
       break;
-    default:  // level 2, its fix-up, the redo pass
+    }
+    default: {  // level 2, its fix-up, the redo pass
+      const uint32_t B = (K + 1023) / 1024;
       for (int pass = 0; pass < 2; ++pass) {
-        hipLaunchKernelGGL(k_rbin2<1024>, dim3(a.num_cu), dim3(1024), rbin2_lds(), st, a.S, a.F, a.tb, a.meta, a.rec32,
-                           a.rec16, a.sumfix, pass);
-        if (pass == 0) hipLaunchKernelGGL(k_rfix2, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.kprev);
+        hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(2 * a.num_cu), dim3(B2_NT), rbin2_lds(), st, a.S, a.F, a.tb, a.meta,
+                           a.rec32, a.rec16, a.sumfix, pass);
+        if (pass == 0) {
+          hipLaunchKernelGGL(k_rfix2a, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.kprev);
+          hipLaunchKernelGGL(k_rfix2b, dim3(B), dim3(1024), 0, st, a.F, a.meta);
+        }
       }
       break;
+    }
   }
   return hipGetLastError();
 }

@@ -57,7 +57,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
-constexpr uint32_t ITEM2 = 16384;   // level-1 records per level-2 item
+constexpr uint32_t ITEM2 = 8192;    // level-1 records per level-2 item
 constexpr uint32_t MAX_ITEMS2 = (1u << 30) / ITEM2 + 513;
 struct MetaLayout {
   uint32_t K;
@@ -73,7 +73,8 @@ struct MetaLayout {
   __host__ __device__ constexpr uint32_t btot() const { return 3 * K + 5376; }       // [1024] exact bin totals
   __host__ __device__ constexpr uint32_t hdr() const { return 3 * K + 6400; }        // [64] header (H_*)
   __host__ __device__ constexpr uint32_t istart() const { return 3 * K + 6464; }     // [513] level-2 items per super-tile
-  __host__ __device__ constexpr uint32_t imap() const { return 3 * K + 6980; }       // u16 [MAX_ITEMS2] item -> super-tile
+  __host__ __device__ constexpr uint32_t wsum() const { return 3 * K + 6980; }       // u64 [64] per-workgroup key sums
+  __host__ __device__ constexpr uint32_t imap() const { return 3 * K + 7108; }       // u16 [MAX_ITEMS2] item -> super-tile
   __host__ __device__ constexpr uint32_t words() const { return imap() + MAX_ITEMS2 / 2 + 1; }
 };
 __host__ __device__ constexpr MetaLayout meta_layout(uint32_t F) { return MetaLayout{2 * F}; }

@@ -369,22 +369,86 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
     for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
   }
-  __syncthreads();
-  for (uint32_t item = blockIdx.x; item < cold_items; item += gridDim.x) {
-    const uint32_t t = plan.cold_tile[item];
-    const bool dc = (plan.tile_flags[t] & TF_DIRTY) != 0;
-    if (threadIdx.x < TILE) {  // the tile's sumfix entries (read and cleared here)
+  // the next item, fetched during this item's emission (its latency hides behind the
+  // dense stores): tile, dirty flag, sumfix entry, and -- one pending segment, the
+  // common case -- both halves' key ranges and each thread's first 16-B group of them
+  const bool one = segs.n == 1;
+  uint32_t t = 0;
+  bool dirty = false;
+  int64_t f = 0;
+  KeyRange q0{}, q1{};
+  uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
+  auto fetch = [&](uint32_t it) {
+    if (it >= cold_items) return;
+    t = plan.cold_tile[it];
+    dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;
+    if (threadIdx.x < TILE) {
       const uint32_t s = t * TILE + threadIdx.x;
-      int64_t f = 0;
+      f = 0;
       if (s < st.S) {
         f = st.sumfix[s];
         if (f) st.sumfix[s] = 0;
       }
-      fixl[threadIdx.x] = f;
     }
-    count_tile<NT>(segs, F, t, lut2, hist_add, sum_add);
+    if (one) {
+      q0 = seg_key(segs, 0, F, t, 0);
+      q1 = seg_key(segs, 0, F, t, 1);
+      const uint32_t g = threadIdx.x;
+      if (q0.r32) {
+        x0 = 4 * g < q0.e - q0.a ? reinterpret_cast<const uint4*>(q0.r32 + q0.a)[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        x1 = 4 * g < q1.e - q1.a ? reinterpret_cast<const uint4*>(q1.r32 + q1.a)[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
+      } else {
+        x0 = 8 * g < q0.e - q0.a ? reinterpret_cast<const uint4*>(q0.r16 + q0.a)[g] : make_uint4(0u, 0u, 0u, 0u);
+        x1 = 8 * g < q1.e - q1.a ? reinterpret_cast<const uint4*>(q1.r16 + q1.a)[g] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  };
+  fetch(blockIdx.x);
+  __syncthreads();
+  for (uint32_t item = blockIdx.x; item < cold_items; item += gridDim.x) {
+    const uint32_t tc = t;
+    const bool dc = dirty;
+    if (threadIdx.x < TILE) fixl[threadIdx.x] = f;
+    if (one) {
+      // group g of both halves: the prefetched first one, then g + NT, ...
+      const uint32_t n0 = q0.e - q0.a, n1 = q1.e - q1.a;
+      if (q0.r32) {
+        const uint32_t g0 = (n0 + 3) / 4, g1 = (n1 + 3) / 4, gm = max(g0, g1);
+        const uint4* p0 = reinterpret_cast<const uint4*>(q0.r32 + q0.a);
+        const uint4* p1 = reinterpret_cast<const uint4*>(q1.r32 + q1.a);
+        uint4 x = x0, y = x1;
+        for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+          uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (4 * g + k >= n0) v[k] = 0xFFFFFFFFu;
+            if (4 * g + k >= n1) v[4 + k] = 0xFFFFFFFFu;
+          }
+          const uint32_t gn = g + NT;
+          x = gn < g0 ? p0[gn] : make_uint4(~0u, ~0u, ~0u, ~0u);
+          y = gn < g1 ? p1[gn] : make_uint4(~0u, ~0u, ~0u, ~0u);
+          count_batch<8>(v, lut2, hist_add, sum_add);
+        }
+      } else {
+        const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
+        const uint4* p0 = reinterpret_cast<const uint4*>(q0.r16 + q0.a);
+        const uint4* p1 = reinterpret_cast<const uint4*>(q1.r16 + q1.a);
+        uint4 x = x0, y = x1;
+        for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+          const uint4 cx = x, cy = y;
+          const uint32_t gn = g + NT;
+          x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
+          y = gn < g1 ? p1[gn] : make_uint4(0u, 0u, 0u, 0u);
+          count16(cx, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
+          count16(cy, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
+        }
+      }
+    } else {
+      count_tile<NT>(segs, F, tc, lut2, hist_add, sum_add);
+    }
     __syncthreads();  // counts complete; fixl visible
-    const uint32_t s0 = t * TILE;
+    fetch(item + gridDim.x);
+    const uint32_t s0 = tc * TILE;
     // linear emission: a clean whole tile inside the output range of a resetting
     // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
     // of 14384 16-B chunks by the whole workgroup in step -- 5.6 TB/s against 4.1 for
@@ -433,7 +497,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
         o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
       }
     }
-    if (threadIdx.x == 0) st.dirty[t] = keep ? 1 : 0;
+    if (threadIdx.x == 0) st.dirty[tc] = keep ? 1 : 0;
     __syncthreads();  // rows cleared, fixl consumed
   }
 }

@@ -268,6 +268,14 @@ class HistogramEngine:
                     "l5dh_merge")
         return (first.value, count.value, out[:count.value]) if own else (first.value, count.value)
 
+    def tile_totals(self) -> np.ndarray:
+        """l5dh_tile_totals: records per 32-series tile of the last binned batch."""
+        F = (self.max_series + 31) // 32
+        out = np.zeros(F, np.uint64)
+        self._check(self._lib.l5dh_tile_totals(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), F),
+                    "l5dh_tile_totals")
+        return out
+
     def merge_bytes(self) -> dict:
         """l5dh_merge_bytes: dense / encoded / sent bytes of the last merge."""
         d, e, s = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)

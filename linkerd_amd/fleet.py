@@ -54,6 +54,74 @@ def shard_ranges(total_series: int, world: int, weights: Optional[np.ndarray] = 
     return [Shard(r, bounds[r], bounds[r + 1] - bounds[r]) for r in range(world)]
 
 
+@dataclass(frozen=True)
+class CostModel:
+    """Modelled device time (ms) of one snapshot interval of a series range on one
+    MI355X: `per_sample` for a sample partitioned at ingest and accumulated at the
+    snapshot, `per_series` for a series' dense row + summary (7.2 KB written), and
+    `per_sample_fold` for a range of at most one tile (32 series), which is folded
+    into its state rows at ingest (k_fold1); `fixed` = launches and plans.  One model
+    for any series count and sample count (bench.py fits it to measured C3 / C2 / C1
+    steps)."""
+    per_sample: float
+    per_series: float
+    per_sample_fold: float
+    fixed: float
+
+    def range_ms(self, samples: float, series: int) -> float:
+        if series <= 32:
+            return self.fixed + self.per_sample_fold * samples + self.per_series * series
+        return self.fixed + self.per_sample * samples + self.per_series * series
+
+
+def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard]:
+    """Contiguous series ranges of equal modelled device time, from the previous
+    interval's records per 32-series tile (l5dh_tile_totals of the rank that held
+    them, or an expected load): a tile's records are spread evenly over its series
+    for the boundaries.  When the first tile alone, folded at ingest, costs less than
+    the slowest rank of the plain split, rank 0 takes exactly that tile and the other
+    ranks split the rest (a Zipf head concentrates there)."""
+    t = np.asarray(tile_samples, dtype=np.float64)
+    F = (S + 31) // 32
+    if t.size != F:
+        raise ValueError(f"tile_samples must hold {F} tiles")
+    per_series = np.repeat(t / 32.0, 32)[:S]
+    w = cost.per_sample * per_series + cost.per_series
+    plain = shard_ranges(S, world, weights=w)
+    if world == 1 or S <= 32:
+        return plain
+
+    def ms(x: Shard) -> float:
+        return cost.range_ms(float(per_series[x.first:x.first + x.count].sum()), x.count) if x.count else 0.0
+
+    rest = shard_ranges(S - 32, world - 1, weights=w[32:])
+    pinned = [Shard(0, 0, 32)] + [Shard(x.rank + 1, x.first + 32, x.count) for x in rest]
+    if max(ms(x) for x in pinned) < max(ms(x) for x in plain):
+        return pinned
+    return plain
+
+
+def plan_ms(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) -> List[float]:
+    """Modelled device time (ms) of every rank of a plan."""
+    t = np.asarray(tile_samples, dtype=np.float64)
+    per_series = np.repeat(t / 32.0, 32)[:S]
+    return [cost.range_ms(float(per_series[x.first:x.first + x.count].sum()), x.count) if x.count else 0.0
+            for x in shards]
+
+
+def plan_spread(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) -> float:
+    """max / min modelled rank time of a plan (1.0 = perfectly balanced).  A pinned
+    one-tile rank 0 (plan_shards) cannot take more work without losing its fold, so
+    it only has to stay at or below the others' maximum; the spread is of the rest."""
+    ms = plan_ms(shards, tile_samples, S, cost)
+    if len(shards) > 1 and shards[0].count <= 32 < S:
+        if ms[0] > max(ms[1:]):
+            return ms[0] / min(ms[1:])
+        ms = ms[1:]
+    ms = [m for m in ms if m > 0]
+    return max(ms) / min(ms)
+
+
 class SeriesRouter:
     """Routes a COO batch of global series ids to the owning ranks (local ids)."""
 

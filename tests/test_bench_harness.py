@@ -30,32 +30,37 @@ def test_c3_ranks_cover_the_series_space(gpus):
         assert b["base_index"] == a["base_index"] + a["samples"]
     assert plans[-1]["first"] + plans[-1]["count"] == 1_000_000
     assert sum(p["samples"] for p in plans) == 1_000_000_000
-    # equal modelled device time per rank (bench.shard_cost), within 2 %
+    # equal modelled device time per rank (fleet.plan_shards over the expected tile load), within 3 %
     sys.path.insert(0, REPO)
     import bench
-    from linkerd_amd import synth
-    w = bench.shard_cost(synth.zipf_cdf(1_000_000), 1_000_000_000, gpus)
-    cost = [w[p["first"]:p["first"] + p["count"]].sum() for p in plans]
-    assert max(cost) / min(cost) < 1.02
-
-
-def test_c3_eight_way_plan_pins_the_folded_first_tile():
-    """8 ranks: rank 0 holds exactly the first tile (one tile is folded at ingest,
-    k_fold1), the other 7 split the rest with equal modelled device time; 2 and 4
-    ranks keep a partitioned head shard."""
-    sys.path.insert(0, REPO)
-    import bench
-    from linkerd_amd import synth
+    from linkerd_amd import fleet, synth
     cdf = synth.zipf_cdf(1_000_000)
-    sh = bench.shard_plan(1_000_000, 1_000_000_000, 8, cdf)
-    assert (sh[0].first, sh[0].count) == (0, bench.ONE_TILE)
-    assert sum(x.count for x in sh) == 1_000_000 and all(b.first == a.first + a.count for a, b in zip(sh, sh[1:]))
-    w = bench.shard_cost(cdf, 1_000_000_000, 8)
-    cost = [w[x.first:x.first + x.count].sum() for x in sh[1:]]
-    assert max(cost) / min(cost) < 1.02
-    assert bench.COST_FIRST_TILE_FOLDED < min(cost)
-    for world in (2, 4):
-        assert bench.shard_plan(1_000_000, 1_000_000_000, world, cdf)[0].count > bench.ONE_TILE
+    load = bench.expected_tile_load(cdf, 1_000_000_000)
+    shards = [fleet.Shard(p["rank"], p["first"], p["count"]) for p in plans]
+    assert fleet.plan_spread(shards, load, 1_000_000, fleet.CostModel(**bench.C3_COST)) < 1.03
+
+
+def test_c3_plan_is_load_derived_for_any_size():
+    """One cost model for any (S, N): the plan comes from per-tile loads (no table tied
+    to C3), and balances C3 and other sizes alike."""
+    sys.path.insert(0, REPO)
+    import bench
+    import numpy as np
+    from linkerd_amd import fleet, synth
+    cost = fleet.CostModel(**bench.C3_COST)
+    assert not [n for n in dir(bench) if n.startswith("COST_CALIBRATION")]
+    for S, N, world in ((1_000_000, 1_000_000_000, 8), (1_000_000, 1_000_000_000, 4), (300_000, 200_000_000, 8),
+                        (50_000, 10_000_000, 2)):
+        cdf = synth.zipf_cdf(S)
+        load = bench.expected_tile_load(cdf, N)
+        sh = bench.shard_plan(S, N, world, cdf)
+        assert sum(x.count for x in sh) == S and all(b.first == a.first + a.count for a, b in zip(sh, sh[1:]))
+        assert fleet.plan_spread(sh, load, S, cost) < 1.03, (S, N, world)
+    # a measured load (l5dh_tile_totals of the previous interval) plans the same way
+    rng = np.random.default_rng(0)
+    load = rng.poisson(bench.expected_tile_load(synth.zipf_cdf(100_000), 50_000_000)).astype(np.uint64)
+    sh = fleet.plan_shards(load, 100_000, 4, cost)
+    assert fleet.plan_spread(sh, load, 100_000, cost) < 1.03
 
 
 def test_c4_ranks_split_the_samples():
