@@ -383,9 +383,13 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   }
   if (int r = ensure(c, c->split_item, (recs / hc + 2 * (size_t)c->F + 2) * 8)) return r;
   Plan pl = plan(c);
+  // a resetting snapshot of every series into dense rows: clean big tiles count
+  // straight into their output rows (no copy of state rows in k_hot_finish), and those
+  // whose halves are one item each are written by their items alone (TF_SOLO)
+  const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S;
   {
     KTimer kt(c, L5DH_K_SCAN);
-    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, hc, c->d_dirty, pl, c->stream));
+    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, hc, c->d_dirty, direct_out, pl, c->stream));
   }
   // The accumulate kernels are persistent and read their item counts from the plan
   // header on the device, so no host round trip separates them from the plan: the
@@ -394,9 +398,6 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   const uint32_t split_items = (uint32_t)std::min<size_t>(0xFFFFFFF0u, recs / hc + 2 * (size_t)hot);
   State st = state(c);
   Tables tb = tables(c);
-  // a resetting snapshot of every series into dense rows: clean big tiles count
-  // straight into their output rows (no copy of state rows in k_hot_finish)
-  const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S;
   if (hot) {
     KTimer kt(c, L5DH_K_HOT);
     HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, c->stream));
@@ -475,8 +476,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   // region buffers: the plan sizes the regions from the previous batch and a sample
   // of this one, with slack; a plan that does not fit is scaled to these sizes (an
   // overflowing region is then redone with exact sizes, which always fit)
-  const size_t cap32 = n + n / 4 + ((size_t)1 << 19);
-  const size_t cap16 = n + n / 4 + (size_t)64 * 2 * c->F;
+  const size_t cap32 = n + n / 2 + ((size_t)1 << 19);
+  const size_t cap16 = n + n / 2 + (size_t)64 * 2 * c->F;
   {
     int r = ensure(c, sg.rec32, (cap32 + 16) * 4);  // readers load whole 16-B groups
     if (!r) r = ensure(c, sg.rec16, (cap16 + 16) * 2);

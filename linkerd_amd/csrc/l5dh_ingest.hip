@@ -36,20 +36,27 @@ constexpr uint32_t INVALID = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
-// Region capacity of a bin or key: the larger of the previous batch's exact records
-// (+1/16 + 4 sigma) and this batch's sample estimate (+4 sigma), plus a pad; exact
-// when the sample was the whole batch.  A region that still overflows is redone
-// with exact sizes (k_rfix1 / k_rfix2), so this only has to be right almost always.
-// `pct` scales the result (L5DH_PARAM_REGION_PCT; below 100 forces the redo path).
+// Region capacity of a bin or key from the previous batch's exact records `prev`
+// and this batch's sampled ids `e` (scale s = samples per draw): when the sample is
+// consistent with the previous batch (e within 4 sigma above prev / s) the previous
+// count +1/16 + 4 sigma; when it is not (a key that grew, or one never seen) the
+// sample's estimate + 4 sigma; exact when the sample was the whole batch.  Plus a
+// pad.  A region that still overflows is redone with exact sizes (k_rfix1 /
+// k_rfix2), so this only has to be right almost always -- but taking the larger of
+// both bounds always would oversize every key by the sample's 4 sigma (C2: 1.3x, past
+// the region buffer).  `pct` scales the result (L5DH_PARAM_REGION_PCT; below 100
+// forces the redo path).
 __device__ __forceinline__ uint32_t rcap(double prev, double e, double s, bool exact, double pad, uint32_t align,
                                          uint32_t pct) {
   double c;
   if (exact) {
     c = e;
   } else {
-    const double a = prev > 0.0 ? prev * 1.0625 + 4.0 * sqrt(prev) : 0.0;
-    const double b = (e + 4.0 * sqrt(e + 1.0)) * s;
-    c = ceil(fmax(a, b)) + pad;
+    const double e0 = prev / s;
+    if (prev > 0.0 && e <= e0 + 4.0 * sqrt(e0 + 1.0))
+      c = ceil(prev * 1.0625 + 4.0 * sqrt(prev)) + pad;
+    else
+      c = ceil((e + 4.0 * sqrt(e + 1.0)) * s) + pad;
   }
   if (pct != 100) c = floor(c * (double)pct / 100.0);
   return round_up((uint32_t)fmin(c, 1073741824.0), align);
@@ -562,18 +569,14 @@ __global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restri
     meta[L.kcnt() + k] = 0u;
   }
   if (blockIdx.x != 0) return;  // (workgroup-uniform)
-  // level-2 items of super-tile j = thread
+  // level-2 items of super-tile j = thread (k_rbin2 finds an item's super-tile in istart)
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t j = threadIdx.x;
   const uint32_t tot = j < FS ? meta[L.btot() + j] : 0u;
   const uint32_t ni = (tot + ITEM2 - 1) / ITEM2;
   uint32_t all;
   const uint32_t is = block_excl_scan<1024>(ni, lds, &all);
-  uint16_t* imap = reinterpret_cast<uint16_t*>(meta + L.imap());
-  if (j < FS) {
-    meta[L.istart() + j] = is;
-    for (uint32_t q = 0; q < ni; ++q) imap[is + q] = (uint16_t)j;
-  }
+  if (j < FS) meta[L.istart() + j] = is;
   if (j == 0) {
     meta[L.istart() + FS] = all;
     hdr[H_ITEMS] = all;
@@ -583,28 +586,33 @@ __global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restri
 }
 
 // ------------------------------------------------------------------------
-// Level 2 (persistent): workgroup w walks items [w I / G, (w + 1) I / G) -- item
-// order is super-tile order, so a workgroup sees few super-tiles and folds the
-// value sums of one super-tile's 2048 series in LDS (u64), flushed to sumfix when
-// it moves on.  Per item (<= ITEM2 level-1 records, 16 per thread): bucket (LUT),
-// 16-bit record, key = 2 tile-in-ST + half; LDS counting sort by key, one returning
-// global atomic per non-empty key on its cursor, stage {rec16 | key << 16}, written
-// in order to run base + position.
+// Level 2 (persistent, one 1024-thread workgroup per CU): workgroup w walks items
+// [w I / G, (w + 1) I / G) -- item order is super-tile order, so a workgroup sees
+// few super-tiles and folds the value sums of one super-tile's 2048 series in LDS
+// (u64), flushed to sumfix when it moves on.  Per item (<= ITEM2 level-1 records,
+// 16 per thread): bucket (LUT), 16-bit record, key = 2 tile-in-ST + half; LDS
+// counting sort by key, one returning global atomic per non-empty key on its
+// cursor, stage {rec16 | key << 16}, written in order to run base + position.
+// Software pipeline, so no global latency is waited for in the item loop: the
+// next item's records are loaded while this one is processed, and the stage and
+// run offsets are double-buffered -- item i's cursor atomics are issued before its
+// scatter and the write-out of item i - 1, and read after them.
 constexpr int B2_KEYS = 2 * ST_TILES;
-constexpr int B2_NT = 512;  // two workgroups per CU: one's loads and atomics overlap the other's LDS phases
-constexpr size_t rbin2_lds() { return (size_t)ITEM2 * 3 + 2048 * 8 + LUT2_N * 8 + B2_KEYS * 12 + 16; }
+constexpr int B2_NT = 1024;
+constexpr size_t rbin2_lds() { return 2048 * 8 + LUT2_N * 8 + 2 * B2_KEYS * 8 + B2_KEYS * 4 + 2 * (size_t)ITEM2 * 4; }
 
 template <int NT>
-__global__ __launch_bounds__(NT, 4) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
+__global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
                                                  const uint32_t* __restrict__ rec32, uint16_t* __restrict__ rec16,
                                                  int64_t* __restrict__ sumfix, int pass) {
+  constexpr int PT = (int)ITEM2 / NT;
+  constexpr int PG = PT / 4;  // 16-B groups per thread
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem);             // [2048]
-  uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                                // [LUT2_N]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);                         // [B2_KEYS]
-  uint2* ocx = reinterpret_cast<uint2*>(cnt + B2_KEYS);                               // [B2_KEYS]
-  uint16_t* stage = reinterpret_cast<uint16_t*>(ocx + B2_KEYS);                       // [ITEM2] rec16, sorted
-  uint8_t* stagek = reinterpret_cast<uint8_t*>(stage + ITEM2);                        // [ITEM2] their keys
+  unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem);  // [2048]
+  uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                     // [LUT2_N]
+  uint2* ocx = lut2 + LUT2_N;                                              // [2][B2_KEYS] {stage offset, run base}
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(ocx + 2 * B2_KEYS);          // [B2_KEYS]
+  uint32_t* stage = cnt + B2_KEYS;                                         // [2][ITEM2] {rec16 | key << 16}, sorted
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO2]) == 0u) return;
@@ -612,14 +620,46 @@ __global__ __launch_bounds__(NT, 4) void k_rbin2(uint32_t S, uint32_t F, Tables 
   const uint32_t i0 = (uint32_t)(((uint64_t)blockIdx.x * nitems) / gridDim.x);
   const uint32_t i1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * nitems) / gridDim.x);
   if (i0 >= i1) return;
-  const uint16_t* imap = reinterpret_cast<const uint16_t*>(meta + L.imap());
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   uint32_t* kcnt = meta + L.kcnt();
   const uint32_t* kbase = meta + L.kbase();
   const uint32_t* kcap = meta + L.kcap();
+  const uint32_t* m_is = meta + L.istart();  // [FS + 1] first item of each super-tile (wave-uniform reads)
+  const uint32_t* m_bb = meta + L.bbase();   // level-1 region base
+  const uint32_t* m_bt = meta + L.btot();    // level-1 records
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
   for (int i = threadIdx.x; i < 2048; i += NT) lsum[i] = 0ull;
   for (int i = threadIdx.x; i < B2_KEYS; i += NT) cnt[i] = 0u;
+  // super-tile of the first item: the last j with istart[j] <= i0 (empty super-tiles
+  // share their successor's start)
+  uint32_t jl = 0, jh = FS;  // istart[jl] <= i0 < istart[jh]
+  while (jh - jl > 1) {
+    const uint32_t mid = (jl + jh) >> 1;
+    if (m_is[mid] <= i0) jl = mid; else jh = mid;
+  }
+  __syncthreads();
+  // item -> [a, e) of its super-tile's level-1 region (a is 4-aligned)
+  uint32_t jn = jl;
+  auto item_range = [&](uint32_t item, uint32_t& j, uint32_t& a, uint32_t& e) {
+    while (m_is[jn + 1] <= item) ++jn;
+    j = jn;
+    const uint32_t bb = m_bb[jn];
+    a = bb + (item - m_is[jn]) * ITEM2;
+    e = min(a + ITEM2, bb + m_bt[jn]);
+  };
+  auto load = [&](uint32_t a, uint32_t e, uint4 (&x)[PG]) {
+#pragma unroll
+    for (int g = 0; g < PG; ++g) {
+      const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x);
+      x[g] = idx < e ? *reinterpret_cast<const uint4*>(rec32 + idx) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      if (idx + 4u > e) {  // the group straddling the region's end: its tail is not this region's
+        if (idx + 1u >= e) x[g].y = ~0u;
+        if (idx + 2u >= e) x[g].z = ~0u;
+        if (idx + 3u >= e) x[g].w = ~0u;
+      }
+    }
+  };
   uint32_t cur_j = 0xFFFFFFFFu;
   auto flush = [&](uint32_t jj) {  // the super-tile's value sums into sumfix (one atomic per nonzero series)
     for (int i = threadIdx.x; i < 2048; i += NT) {
@@ -629,102 +669,126 @@ __global__ __launch_bounds__(NT, 4) void k_rbin2(uint32_t S, uint32_t F, Tables 
       lsum[i] = 0ull;
     }
   };
-  constexpr int PG = ITEM2 / 4 / NT;  // 16-B groups per thread
-  for (uint32_t item = i0; item < i1; ++item) {
-    const uint32_t j = imap[item];
-    const uint32_t q = item - meta[L.istart() + j];
-    const uint32_t a = meta[L.bbase() + j] + q * ITEM2;  // 4-aligned
-    const uint32_t e = min(a + ITEM2, meta[L.bbase() + j] + meta[L.btot() + j]);
-    uint4 x[PG];
-#pragma unroll
-    for (int g = 0; g < PG; ++g) {
-      const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x);
-      x[g] = idx < e ? *reinterpret_cast<const uint4*>(rec32 + idx) : make_uint4(0u, 0u, 0u, 0u);
-    }
-    if (j != cur_j) {
-      __syncthreads();  // the previous item's write-out has read the stage
-      if (pass == 0 && cur_j != 0xFFFFFFFFu) flush(cur_j);
-      cur_j = j;
-      __syncthreads();
-    }
-    // {rec16 | key << 16} of slot k of group g (~0u: no record); decoded twice -- here
-    // for the ranks and the sums, after the scan for the stage -- to keep the
-    // records (x) and ranks in registers without spilling
-    auto decode = [&](int g, int k, uint32_t r, bool sums) -> uint32_t {
-      const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x) + (uint32_t)k;
-      const uint32_t p = r & 0x1FFFFFu;
-      uint32_t o;
-      const uint32_t b = lut2_decode(p, lut2[lut2_index(p)], o);
-      const bool esc = p >= V_ESC;
-      const uint32_t bucket = sel_u32(esc, p - V_ESC, b);
-      const uint32_t sl = (r >> 21) & 31u, tl = r >> 26;
-      if (idx >= e) return NOKEY;
-      if (sums && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
-      return (sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16);
-    };
-    uint32_t rank[4 * PG];
-#pragma unroll
-    for (int g = 0; g < PG; ++g) {
-      const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t kr = decode(g, k, xs[k], pass == 0);
-        rank[4 * g + k] = kr != NOKEY ? atomicAdd(&cnt[kr >> 16], 1u) : 0u;
+  // write-out of a sorted stage (each wave a contiguous range)
+  auto write_out = [&](int bb, uint32_t total) {
+    const uint32_t* st = stage + bb * ITEM2;
+    const uint2* oc = ocx + bb * B2_KEYS;
+#pragma unroll 4
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
+      if (i < total) {
+        const uint32_t x = st[i];
+        const uint2 o = oc[x >> 16];
+#if defined(L5DH_EXP) && (L5DH_EXP & 4)  // timing only: no run stores
+        if (o.y == 12345u) rec16[o.y + (i - o.x)] = (uint16_t)(x & 0xFFFFu);
+#else
+        if (o.y != INVALID) rec16[o.y + (i - o.x)] = (uint16_t)(x & 0xFFFFu);
+#endif
       }
     }
-    __syncthreads();
-    // run reservations: waves 0 and 1, lane = key; wave 0 also scans the key counts
+  };
+  uint32_t j, a, e;
+  item_range(i0, j, a, e);
+  uint4 x[PG];
+  load(a, e, x);
+  uint32_t prev_total = 0;
+  for (uint32_t item = i0; item < i1; ++item) {
+    const int b = (int)(item & 1u);
+    const uint32_t cj = j, ctot = e - a;
+    // (A) the next item's records in flight
+    uint4 xn[PG];
+    if (item + 1 < i1) {
+      item_range(item + 1, j, a, e);
+      load(a, e, xn);
+    }
+    if (cj != cur_j) {
+      if (pass == 0 && cur_j != 0xFFFFFFFFu) {
+        __syncthreads();  // every lane's sums of the previous super-tile are in
+        flush(cur_j);
+      }
+      cur_j = cj;
+      __syncthreads();
+    }
+    // (B) bucket, 16-bit record, key; rank in the key's count; value sums
+    uint32_t kr[PT], rank[PT];
+    {
+      uint32_t r[PT];
+#pragma unroll
+      for (int g = 0; g < PG; ++g) {
+        r[4 * g] = x[g].x; r[4 * g + 1] = x[g].y; r[4 * g + 2] = x[g].z; r[4 * g + 3] = x[g].w;
+      }
+      constexpr int H = PT / 2;  // LUT reads batched per half (bounded register pressure)
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        uint2 lv[H];
+        if (k % H == 0) {
+#pragma unroll
+          for (int q = 0; q < H; ++q) lv[q] = lut2[lut2_index(r[k + q] & 0x1FFFFFu)];
+        }
+        const uint32_t p = r[k] & 0x1FFFFFu;
+        uint32_t o;
+        const uint32_t bk = lut2_decode(p, lv[k % H], o);
+        const bool esc = p >= V_ESC;
+        const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
+        const uint32_t sl = (r[k] >> 21) & 31u, tl = r[k] >> 26;
+        const bool valid = r[k] != 0xFFFFFFFFu;  // (a level-1 record is never ~0: its payload < 2^21 - 1)
+        kr[k] = valid ? ((sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16)) : NOKEY;
+        rank[k] = valid ? atomicAdd(&cnt[kr[k] >> 16], 1u) : 0u;
+#if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only (tools/mk_var.sh): no value sums
+        (void)tl;
+#elif defined(L5DH_EXP) && (L5DH_EXP & 8)  // timing only: u32 value sums
+        if (pass == 0 && valid && !esc && p) atomicAdd(reinterpret_cast<uint32_t*>(lsum) + tl * 32u + sl, p);
+#else
+        if (pass == 0 && valid && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
+#endif
+      }
+    }
+    __syncthreads();  // B1: counts complete
+    // (C) run reservations (waves 0 and 1, lane = key; results read in (F)); wave 2
+    // scans the counts into this item's stage offsets
     uint32_t rc = 0, rold = 0, rbase = 0, rcapv = 0;
     const uint32_t rk = (uint32_t)wv * 64u + (uint32_t)lane;
-    const uint32_t gk = j * (uint32_t)B2_KEYS + rk;
     if (wv < 2) {
+      const uint32_t gk = cj * (uint32_t)B2_KEYS + rk;
       rc = cnt[rk];
       if (rc) {
         rold = atomicAdd(&kcnt[gk], rc);
         rbase = kbase[gk];
         rcapv = kcap[gk];
       }
-    }
-    if (wv == 0) {
+    } else if (wv == 2) {
       const uint32_t c0 = cnt[2 * lane], c1 = cnt[2 * lane + 1];
       const uint32_t ex = wave_incl_scan32(c0 + c1) - (c0 + c1);
-      ocx[2 * lane].x = ex;
-      ocx[2 * lane + 1].x = ex + c0;
+      ocx[b * B2_KEYS + 2 * lane].x = ex;
+      ocx[b * B2_KEYS + 2 * lane + 1].x = ex + c0;
     }
-    __syncthreads();
+    __syncthreads();  // B2: stage offsets visible; every count read
+    // (D) scatter this item into its stage
+    {
+      uint32_t* st = stage + b * ITEM2;
+      const uint2* oc = ocx + b * B2_KEYS;
 #pragma unroll
-    for (int g = 0; g < PG; ++g) {
-      const uint32_t xs[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t kr = decode(g, k, xs[k], false);
-        if (kr != NOKEY) {
-          const uint32_t pos = ocx[kr >> 16].x + rank[4 * g + k];
-          stage[pos] = (uint16_t)(kr & 0xFFFFu);
-          stagek[pos] = (uint8_t)(kr >> 16);
-        }
-      }
+      for (int k = 0; k < PT; ++k)
+        if (kr[k] != NOKEY) st[oc[kr[k] >> 16].x + rank[k]] = kr[k];
     }
+    // (E) write-out of the previous item (its stage and run offsets are complete)
+    if (item > i0) write_out(b ^ 1, prev_total);
+    // (F) this item's run bases; counts cleared for the next item
     if (wv < 2) {
       uint32_t rb = INVALID;
       if (rc) {
         if (rold + rc <= rcapv) rb = rbase + rold;
         else hdr[H_OV2] = 1u;  // dropped; k_rfix2 has level 2 redone with exact regions
       }
-      ocx[rk].y = rb;
+      ocx[b * B2_KEYS + rk].y = rb;
       cnt[rk] = 0u;
     }
-    __syncthreads();
-    const uint32_t total = e - a;
+    __syncthreads();  // B3
+    prev_total = ctot;
 #pragma unroll
-    for (int k = 0; k < 4 * PG; ++k) {  // each wave a contiguous range of the stage
-      const uint32_t i = (uint32_t)wv * (4 * PG * 64) + (uint32_t)k * 64 + (uint32_t)lane;
-      if (i < total) {
-        const uint2 o = ocx[stagek[i]];
-        if (o.y != INVALID) rec16[o.y + (i - o.x)] = stage[i];
-      }
-    }
+    for (int g = 0; g < PG; ++g) x[g] = xn[g];
   }
+  write_out((int)((i1 - 1) & 1u), prev_total);
   __syncthreads();
   if (pass == 0) flush(cur_j);
 }
@@ -838,7 +902,7 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
     default: {  // level 2, its fix-up, the redo pass
       const uint32_t B = (K + 1023) / 1024;
       for (int pass = 0; pass < 2; ++pass) {
-        hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(2 * a.num_cu), dim3(B2_NT), rbin2_lds(), st, a.S, a.F, a.tb, a.meta,
+        hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(a.num_cu), dim3(B2_NT), rbin2_lds(), st, a.S, a.F, a.tb, a.meta,
                            a.rec32, a.rec16, a.sumfix, pass);
         if (pass == 0) {
           hipLaunchKernelGGL(k_rfix2a, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.kprev);

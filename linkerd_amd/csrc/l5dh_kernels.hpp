@@ -57,8 +57,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
-constexpr uint32_t ITEM2 = 8192;    // level-1 records per level-2 item
-constexpr uint32_t MAX_ITEMS2 = (1u << 30) / ITEM2 + 513;
+constexpr uint32_t ITEM2 = 16384;   // level-1 records per level-2 item
 struct MetaLayout {
   uint32_t K;
   __host__ __device__ constexpr uint32_t kbase() const { return 0; }
@@ -74,8 +73,7 @@ struct MetaLayout {
   __host__ __device__ constexpr uint32_t hdr() const { return 3 * K + 6400; }        // [64] header (H_*)
   __host__ __device__ constexpr uint32_t istart() const { return 3 * K + 6464; }     // [513] level-2 items per super-tile
   __host__ __device__ constexpr uint32_t wsum() const { return 3 * K + 6980; }       // u64 [64] per-workgroup key sums
-  __host__ __device__ constexpr uint32_t imap() const { return 3 * K + 7108; }       // u16 [MAX_ITEMS2] item -> super-tile
-  __host__ __device__ constexpr uint32_t words() const { return imap() + MAX_ITEMS2 / 2 + 1; }
+  __host__ __device__ constexpr uint32_t words() const { return 3 * K + 7108; }
 };
 __host__ __device__ constexpr MetaLayout meta_layout(uint32_t F) { return MetaLayout{2 * F}; }
 // header words
@@ -118,6 +116,8 @@ struct State {
 
 constexpr uint8_t TF_SPLIT = 2;    // big tile, accumulated per half
 constexpr uint8_t TF_DIRTY = 4;    // the tile held live counts when k_plan ran
+constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, each half ONE item:
+                                   // k_accum_split writes its output rows and summaries itself
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
@@ -169,7 +169,7 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 
 // ---- snapshot launchers (l5dh_snapshot.hip) ----
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
-                       const uint8_t* dirty, Plan plan, hipStream_t st);
+                       const uint8_t* dirty, int direct_out, Plan plan, hipStream_t st);
 // The accumulate launches take UPPER BOUNDS of their item counts (no host round
 // trip for the plan header): the kernels are persistent and read the exact counts
 // from plan.header on the device.  DEV_COUNT as a count: read it on the device.

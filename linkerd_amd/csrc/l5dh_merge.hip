@@ -13,8 +13,8 @@
 //   k_mcount   words per row
 //   k_menc     the rows' entries at their exclusive word offsets
 //   k_mdecode  summed rows of this rank's slice from every source + HistogramSummary
-#include <hipcub/hipcub.hpp>
-
+//   k_scan_*   u32 word counts -> u64 exclusive offsets (tile sums, one-workgroup
+//              scan of the tile sums, tile scans)
 #include "l5dh_device.hpp"
 #include "l5dh_merge.hpp"
 
@@ -122,17 +122,98 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeSources src, u
   wave_summary(g, lds, totals ? totals[r] : 0, tb.mid, out_summ ? out_summ + r : nullptr);
 }
 
+// Exclusive u64 prefix of n u32 counts in tiles of SCAN_TILE: k_scan_sums writes
+// each tile's sum, k_scan_top (one workgroup) scans the tile sums in place, and
+// k_scan_tiles scans each tile from its offset.  tmp = the tile sums.
+constexpr int SCAN_NT = 256, SCAN_PT = 16, SCAN_TILE = SCAN_NT * SCAN_PT;
+
+__device__ __forceinline__ uint64_t block_scan256(uint64_t v, uint64_t* red /*[5]*/, uint64_t* total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_scan(v);
+  if (lane == 63) red[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (int k = 0; k < SCAN_NT / 64; ++k) {
+      const uint64_t q = red[k];
+      red[k] = acc;
+      acc += q;
+    }
+    red[SCAN_NT / 64] = acc;
+  }
+  __syncthreads();
+  const uint64_t r = red[w] + incl - v;
+  *total = red[SCAN_NT / 64];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(SCAN_NT) void k_scan_sums(const uint32_t* __restrict__ x, uint32_t n,
+                                                       uint64_t* __restrict__ sums) {
+  __shared__ uint64_t red[SCAN_NT / 64 + 1];
+  const uint32_t base = blockIdx.x * (uint32_t)SCAN_TILE + threadIdx.x * SCAN_PT;
+  uint64_t v = 0;
+  for (int k = 0; k < SCAN_PT; ++k) v += base + k < n ? x[base + k] : 0u;
+  uint64_t t;
+  block_scan256(v, red, &t);
+  if (threadIdx.x == 0) sums[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(SCAN_NT) void k_scan_top(uint64_t* __restrict__ sums, uint32_t nt) {
+  __shared__ uint64_t red[SCAN_NT / 64 + 1];
+  uint64_t carry = 0;
+  for (uint32_t c = 0; c < nt; c += SCAN_NT) {
+    const uint32_t i = c + threadIdx.x;
+    const uint64_t v = i < nt ? sums[i] : 0ull;
+    uint64_t t;
+    const uint64_t e = block_scan256(v, red, &t);
+    if (i < nt) sums[i] = carry + e;
+    carry += t;
+  }
+}
+
+__global__ __launch_bounds__(SCAN_NT) void k_scan_tiles(const uint32_t* __restrict__ x, uint32_t n,
+                                                        const uint64_t* __restrict__ sums, uint64_t* __restrict__ out) {
+  __shared__ uint64_t red[SCAN_NT / 64 + 1];
+  const uint32_t base = blockIdx.x * (uint32_t)SCAN_TILE + threadIdx.x * SCAN_PT;
+  uint32_t v[SCAN_PT];
+  uint64_t s = 0;
+  for (int k = 0; k < SCAN_PT; ++k) {
+    v[k] = base + k < n ? x[base + k] : 0u;
+    s += v[k];
+  }
+  uint64_t t;
+  uint64_t e = sums[blockIdx.x] + block_scan256(s, red, &t);
+  for (int k = 0; k < SCAN_PT; ++k) {
+    if (base + k < n) out[base + k] = e;
+    e += v[k];
+  }
+}
+
+hipError_t exclusive_scan_u32_u64(const uint32_t* x, uint32_t n, uint64_t* out, void* tmp, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  uint64_t* sums = static_cast<uint64_t*>(tmp);
+  hipLaunchKernelGGL(k_scan_sums, dim3(nt), dim3(SCAN_NT), 0, st, x, n, sums);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_NT), 0, st, sums, nt);
+  hipLaunchKernelGGL(k_scan_tiles, dim3(nt), dim3(SCAN_NT), 0, st, x, n, (const uint64_t*)sums, out);
+  return hipGetLastError();
+}
+
+size_t scan_tmp_bytes(uint32_t n) { return ((size_t)n / SCAN_TILE + 2) * 8; }
+
 }  // namespace
 
 hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
                        size_t* tmp_bytes, hipStream_t st) {
   if (!tmp) {  // size query of the scan's temporary storage
-    return hipcub::DeviceScan::ExclusiveSum(nullptr, *tmp_bytes, words, offs, (int)nrows + 1, st);
+    *tmp_bytes = scan_tmp_bytes(nrows + 1);
+    return hipSuccess;
   }
   if (nrows) hipLaunchKernelGGL(k_mcount, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, words);
   hipError_t e = hipMemsetAsync(words + nrows, 0, 4, st);  // offs[nrows] = the total
   if (e != hipSuccess) return e;
-  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, words, offs, (int)nrows + 1, st);
+  return exclusive_scan_u32_u64(words, nrows + 1, offs, tmp, st);
 }
 
 hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st) {
@@ -143,7 +224,8 @@ hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* off
 
 hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
                          hipStream_t st) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, words, offs, (int)nrows, st);
+  if (tmp_bytes < scan_tmp_bytes(nrows)) return hipErrorInvalidValue;
+  return exclusive_scan_u32_u64(words, nrows, offs, tmp, st);
 }
 
 hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,

@@ -88,7 +88,8 @@ __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int fina
 }
 
 __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
-                                                 uint32_t hot_chunk, const uint8_t* __restrict__ dirty, Plan plan) {
+                                                 uint32_t hot_chunk, const uint8_t* __restrict__ dirty, int direct_out,
+                                                 Plan plan) {
   __shared__ uint4 lds4[17];
   __shared__ uint32_t base[4];
   __shared__ uint32_t nbig;
@@ -140,6 +141,10 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
     uint8_t flags = dirty[t] ? TF_DIRTY : 0;
     if (c.hot) {
       flags |= TF_SPLIT;
+      // both halves one item each, clean, whole-range resetting snapshot into dense rows:
+      // the items own their 16 output rows (no zeroing, no atomics, no finish pass)
+      const uint32_t h1 = tot - c.h0;
+      if (direct_out && !dirty[t] && c.h0 > 0 && c.h0 <= hot_chunk && h1 > 0 && h1 <= hot_chunk) flags |= TF_SOLO;
       for (uint32_t h = 0; !coop && h < 2; ++h) {
         const uint32_t nh = ((h ? tot - c.h0 : c.h0) + hot_chunk - 1) / hot_chunk;
         for (uint32_t q = 0; q < nh; ++q) plan.split_item[sa++] = make_uint2(t | (h << 15), q);
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(256) void k_hot_init(Plan plan, State st, Outputs o
   const uint32_t nh = plan.header[1];
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const uint32_t t = plan.hot_list[i];
-    if (plan.tile_flags[t] & TF_DIRTY) continue;
+    if (plan.tile_flags[t] & (TF_DIRTY | TF_SOLO)) continue;
     const uint32_t s0 = t * TILE;
     const uint32_t s1 = min(st.S, s0 + TILE);
     if (direct_out) {  // the output rows: (s1 - s0) x 1798 int32, 8-B aligned
@@ -717,7 +722,23 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
     __syncthreads();
     const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
     const uint32_t s = t * TILE + 16 * half + w;
-    if (s < st.S) {
+    if (plan.tile_flags[t] & TF_SOLO) {
+      // this item holds every record of the half: wave w writes series w's output row,
+      // total and summary (direct_out: out.first == 0, the tile is clean, reset)
+      if (s < st.S) {
+        const SrcLds32 src{hist + w * HROW};
+        const int64_t total = (int64_t)my_vsum + st.sumfix[s];
+        uint32_t g[9];
+        row_pass(src, g, out.counts + (size_t)s * NB);
+        wave_summary(g, src, total, tb.mid, out.summ ? out.summ + s : nullptr);
+        if (lane == 0) {
+          st.sumfix[s] = 0;
+          st.total[s] = total;
+          if (out.totals) out.totals[s] = total;
+        }
+      }
+      if (threadIdx.x == 0 && half == 0) st.dirty[t] = 0;
+    } else if (s < st.S) {
       const BigRows br = big_rows(st, out, plan, t, direct_out);
       uint32_t* grow = br.base + (size_t)(16 * half + w) * br.stride;
       const uint32_t* hrow = hist + w * HROW;
@@ -742,6 +763,7 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
   for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
     const uint32_t t = plan.hot_list[vb >> 1];
     const uint32_t half = vb & 1u;
+    if (plan.tile_flags[t] & TF_SOLO) continue;  // written by its k_accum_split items
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t s = t * TILE + 16 * half + w;
@@ -846,10 +868,11 @@ hipError_t set_snapshot_attributes() {
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
-                       const uint8_t* dirty, Plan plan, hipStream_t st) {
+                       const uint8_t* dirty, int direct_out, Plan plan, hipStream_t st) {
   const uint32_t B = (F + 1023) / 1024;  // header holds 4 + 3 B words (l5dh_engine.cpp)
   hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
-  hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, plan);
+  hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty,
+                     direct_out, plan);
   return hipGetLastError();
 }
 

@@ -89,3 +89,19 @@ def test_open_rejects_bad_arguments_without_device(lib):
     assert lib.l5dh_open(ctypes.byref(ctx), 10, 3) == -22         # two devices
     assert lib.l5dh_open(None, 10, 1) == -22
     assert lib.l5dh_close(None) in (0, -22)
+
+
+def test_no_development_switches_in_the_shipped_library(lib):
+    """The shipped library reads no environment (no L5DH_DBG-style switches that
+    would let a host silently skip work) and carries no such string."""
+    data = open(N.LIB_PATH, "rb").read()
+    assert b"L5DH_DBG" not in data
+    nm = shutil.which("nm")
+    if nm:
+        undef = subprocess.run([nm, "-D", "--undefined-only", N.LIB_PATH], capture_output=True, text=True).stdout
+        assert not re.search(r"\b(secure_)?getenv\b", undef), "libl5dhist.so imports getenv"
+    src = os.path.join(REPO, "linkerd_amd", "csrc")
+    for f in os.listdir(src):
+        if f.endswith((".cpp", ".hip", ".hpp")):
+            text = open(os.path.join(src, f)).read()
+            assert "getenv" not in text and "g_dbg" not in text, f

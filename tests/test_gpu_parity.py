@@ -483,3 +483,28 @@ def test_slab_counts_bitexact(oracle, gmax, mode):
     got, counts = eng.snapshot(reset=True, with_counts=True)
     np.testing.assert_array_equal(counts, o.counts())
     _assert_summaries_equal(got, o.snapshot(reset=True), f"gmax={gmax}")
+
+
+@pytest.mark.parametrize("regime", ["default", "redo", "nodirect"])
+def test_tile_totals_are_the_batch_load(regime):
+    """l5dh_tile_totals (the load-derived shard plan's input) = records per 32-series
+    tile of the last binned batch, exactly: invalid ids excluded, direct and level-2
+    tiles alike, after a redo too."""
+    rng = np.random.default_rng(11)
+    S = 70_001
+    F = (S + 31) // 32
+    s, _ = synth.c3(S=S, N=2_000_000, seed=5)
+    s = s.copy()
+    s[:1000] = S + 7  # invalid ids: dropped, not counted
+    v = rng.uniform(0, 5000, s.size).astype(np.float32)
+    e = _engine(S, regime)
+    try:
+        for k in range(2):  # the second batch plans from the first's exact counts
+            try:
+                e.ingest(s, v)
+            except Exception:
+                pass  # the invalid ids are reported (the valid samples are ingested)
+            want = np.bincount(s[s < S] // 32, minlength=F).astype(np.uint64)
+            np.testing.assert_array_equal(e.tile_totals(), want)
+    finally:
+        e.close()

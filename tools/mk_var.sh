@@ -11,6 +11,7 @@ mkdir -p ../lib_ab
 /opt/rocm/bin/hipcc $F -c l5dh_ingest.hip -o $T/i.o &
 /opt/rocm/bin/hipcc $F -c l5dh_snapshot.hip -o $T/s.o &
 /opt/rocm/bin/hipcc $F -x hip -c l5dh_engine.cpp -o $T/e.o &
+/opt/rocm/bin/hipcc $F -c l5dh_merge.hip -o $T/m.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib_ab/lib$N.so $T/i.o $T/s.o $T/e.o -L/opt/rocm/lib -lrccl
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib_ab/lib$N.so $T/i.o $T/s.o $T/m.o $T/e.o -L/opt/rocm/lib -lrccl
 rm -rf $T

@@ -1,0 +1,53 @@
+"""Per-kernel device times (HIP events, L5DH_PARAM_TIMING) of one library build on a
+bench workload, without result checks -- for timing-only development builds
+(tools/mk_var.sh, L5DH_LIB=<lib>).  Development tool (GPU box).
+  L5DH_LIB=... python tools/time_lib.py [--workload c3] [--steps 4]"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    steps = 4
+    argv = sys.argv[1:]
+    if "--steps" in argv:
+        i = argv.index("--steps")
+        steps = int(argv[i + 1])
+        del argv[i:i + 2]
+    sys.argv = ["bench.py"] + argv
+    args = bench.parse()
+    import torch
+    from linkerd_amd import _native as N
+    from linkerd_amd.engine import HistogramEngine
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    pl = bench.plan(args, 1, 0)
+    lib = ctypes.CDLL(N.SYNTH_PATH)
+    for fn in ("l5ds_gen_c1", "l5ds_gen_c2", "l5ds_gen_zipf"):
+        getattr(lib, fn).restype = ctypes.c_int
+    stream = torch.cuda.current_stream().cuda_stream
+    batches = [bench.gen_batch(torch, lib, pl, k, stream) for k in range(2)]
+    S = pl["count"]
+    eng = HistogramEngine(S)
+    eng.set_stream(stream)
+    summ = torch.empty((S, 11), dtype=torch.int64, device="cuda")
+    counts = torch.empty((S, N.NBUCKETS), dtype=torch.int32, device="cuda")
+    for k in range(3):
+        eng.ingest(*batches[k % 2])
+        eng.snapshot_into(summ, counts, reset=True)
+    eng.set_param(N.PARAM_TIMING, 1)
+    eng.kernel_times(reset=True)
+    for k in range(steps):
+        eng.ingest(*batches[k % 2])
+        eng.snapshot_into(summ, counts, reset=True)
+    kt = eng.kernel_times(reset=True)
+    tot = sum(ms for ms, n in kt.values() if n) / steps
+    print(f"{os.path.basename(N.LIB_PATH)}: {tot:.4f} ms/step  " +
+          "  ".join(f"{k} {ms / steps:.4f}" for k, (ms, n) in kt.items() if n), flush=True)
+
+
+if __name__ == "__main__":
+    main()
