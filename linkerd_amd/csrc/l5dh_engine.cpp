@@ -176,7 +176,7 @@ struct l5dh_ctx {
   uint32_t* d_err = nullptr;
   // scratch
   uint32_t* d_tile_tot = nullptr;  // [F] tile totals (snapshot plan)
-  uint32_t* d_cold_tile = nullptr;
+  uint4* d_cold_item = nullptr;
   DevBuf split_item;  // big-tile half chunk items (sized per snapshot)
   uint32_t* d_hot_list = nullptr;
   uint8_t* d_tile_flags = nullptr;
@@ -352,7 +352,7 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot, c->d_cold_tile, static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags,
+  return Plan{c->d_tile_tot, c->d_cold_item, static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags,
               c->d_header};
 }
 
@@ -984,7 +984,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_tile_tot, F * 4) &&
-            mal((void**)&c->d_cold_tile, (F + 1) * 4) && mal((void**)&c->d_hot_list, F * 4) &&
+            mal((void**)&c->d_cold_item, (F + 1) * 16) && mal((void**)&c->d_hot_list, F * 4) &&
             mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) && mal((void**)&c->d_tile_flags, F) &&
             mal((void**)&c->d_kest, 2 * F * 4) && mal((void**)&c->d_kprev, 2 * F * 4);
   const size_t meta_bytes = (size_t)meta_layout((uint32_t)F).words() * 4;
@@ -1031,7 +1031,7 @@ int l5dh_close(l5dh_ctx* c) {
   }
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid,      c->d_base,     c->d_lut,       c->d_lut2,     c->d_counts,
-                  c->d_total,   c->d_sumfix,   c->d_dirty,    c->d_err,       c->d_tile_tot, c->d_cold_tile,
+                  c->d_total,   c->d_sumfix,   c->d_dirty,    c->d_err,       c->d_tile_tot, c->d_cold_item,
                   c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev};
   for (void* p : ptrs)
     if (p) hipFree(p);

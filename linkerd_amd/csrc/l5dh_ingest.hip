@@ -603,8 +603,12 @@ constexpr size_t rbin2_lds() { return 2048 * 8 + LUT2_N * 8 + 2 * B2_KEYS * 8 + 
 
 template <int NT>
 __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
+                                                 const uint32_t* __restrict__ m_is, const uint32_t* __restrict__ m_bb,
+                                                 const uint32_t* __restrict__ m_bt,
                                                  const uint32_t* __restrict__ rec32, uint16_t* __restrict__ rec16,
                                                  int64_t* __restrict__ sumfix, int pass) {
+  // m_is [FS + 1] first item of each super-tile, m_bb level-1 region base, m_bt
+  // level-1 records: words of `meta` this kernel only reads (wave-uniform: scalar loads)
   constexpr int PT = (int)ITEM2 / NT;
   constexpr int PG = PT / 4;  // 16-B groups per thread
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -624,9 +628,6 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
   uint32_t* kcnt = meta + L.kcnt();
   const uint32_t* kbase = meta + L.kbase();
   const uint32_t* kcap = meta + L.kcap();
-  const uint32_t* m_is = meta + L.istart();  // [FS + 1] first item of each super-tile (wave-uniform reads)
-  const uint32_t* m_bb = meta + L.bbase();   // level-1 region base
-  const uint32_t* m_bt = meta + L.btot();    // level-1 records
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
   for (int i = threadIdx.x; i < 2048; i += NT) lsum[i] = 0ull;
@@ -642,22 +643,19 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
   // item -> [a, e) of its super-tile's level-1 region (a is 4-aligned)
   uint32_t jn = jl;
   auto item_range = [&](uint32_t item, uint32_t& j, uint32_t& a, uint32_t& e) {
-    while (m_is[jn + 1] <= item) ++jn;
+    while (m_is[jn + 1] <= item) jn = __builtin_amdgcn_readfirstlane(jn + 1);
     j = jn;
     const uint32_t bb = m_bb[jn];
     a = bb + (item - m_is[jn]) * ITEM2;
     e = min(a + ITEM2, bb + m_bt[jn]);
   };
+  // unconditional loads (a group past the item's end reloads its first group), so all
+  // of them stay in flight; records past the end are masked where they are used
   auto load = [&](uint32_t a, uint32_t e, uint4 (&x)[PG]) {
 #pragma unroll
     for (int g = 0; g < PG; ++g) {
       const uint32_t idx = a + 4u * ((uint32_t)g * NT + threadIdx.x);
-      x[g] = idx < e ? *reinterpret_cast<const uint4*>(rec32 + idx) : make_uint4(~0u, ~0u, ~0u, ~0u);
-      if (idx + 4u > e) {  // the group straddling the region's end: its tail is not this region's
-        if (idx + 1u >= e) x[g].y = ~0u;
-        if (idx + 2u >= e) x[g].z = ~0u;
-        if (idx + 3u >= e) x[g].w = ~0u;
-      }
+      x[g] = *reinterpret_cast<const uint4*>(rec32 + (idx < e ? idx : a));
     }
   };
   uint32_t cur_j = 0xFFFFFFFFu;
@@ -695,12 +693,11 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
   for (uint32_t item = i0; item < i1; ++item) {
     const int b = (int)(item & 1u);
     const uint32_t cj = j, ctot = e - a;
-    // (A) the next item's records in flight
+    // (A) the next item's records in flight (after the last item: this item's again,
+    // unconditionally, so that no copy of the registers waits for the loads)
     uint4 xn[PG];
-    if (item + 1 < i1) {
-      item_range(item + 1, j, a, e);
-      load(a, e, xn);
-    }
+    if (item + 1 < i1) item_range(item + 1, j, a, e);
+    load(a, e, xn);
     if (cj != cur_j) {
       if (pass == 0 && cur_j != 0xFFFFFFFFu) {
         __syncthreads();  // every lane's sums of the previous super-tile are in
@@ -731,7 +728,7 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
         const bool esc = p >= V_ESC;
         const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
         const uint32_t sl = (r[k] >> 21) & 31u, tl = r[k] >> 26;
-        const bool valid = r[k] != 0xFFFFFFFFu;  // (a level-1 record is never ~0: its payload < 2^21 - 1)
+        const bool valid = 4u * ((uint32_t)(k >> 2) * NT + threadIdx.x) + (uint32_t)(k & 3) < ctot;
         kr[k] = valid ? ((sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16)) : NOKEY;
         rank[k] = valid ? atomicAdd(&cnt[kr[k] >> 16], 1u) : 0u;
 #if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only (tools/mk_var.sh): no value sums
@@ -902,8 +899,10 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
     default: {  // level 2, its fix-up, the redo pass
       const uint32_t B = (K + 1023) / 1024;
       for (int pass = 0; pass < 2; ++pass) {
+        const MetaLayout L = meta_layout(a.F);
         hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(a.num_cu), dim3(B2_NT), rbin2_lds(), st, a.S, a.F, a.tb, a.meta,
-                           a.rec32, a.rec16, a.sumfix, pass);
+                           a.meta + L.istart(), a.meta + L.bbase(), a.meta + L.btot(), a.rec32, a.rec16, a.sumfix,
+                           pass);
         if (pass == 0) {
           hipLaunchKernelGGL(k_rfix2a, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.kprev);
           hipLaunchKernelGGL(k_rfix2b, dim3(B), dim3(1024), 0, st, a.F, a.meta);

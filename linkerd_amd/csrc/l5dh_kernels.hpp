@@ -114,6 +114,8 @@ struct State {
   uint32_t S, F;
 };
 
+constexpr uint32_t CI_DIRTY = 1u << 30;  // cold item: the tile held live counts
+constexpr uint32_t CI_R32 = 1u << 31;    // cold item: its records are rec32 (a direct tile)
 constexpr uint8_t TF_SPLIT = 2;    // big tile, accumulated per half
 constexpr uint8_t TF_DIRTY = 4;    // the tile held live counts when k_plan ran
 constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, each half ONE item:
@@ -121,7 +123,8 @@ constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, 
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
-  uint32_t* cold_tile;     // [F] cold item -> tile
+  uint4* cold_item;        // [F] cold item -> {tile | CI_DIRTY | CI_R32, a0, a1, n0 | n1 << 16}: segment 0's
+                           // key ranges of the tile's halves (rec32 records when CI_R32, else rec16)
   uint2* split_item;       // [split items] {tile | half << 15, chunk} of big tiles
   uint32_t* hot_list;      // [F] big tiles
   uint8_t* tile_flags;     // [F] TF_*

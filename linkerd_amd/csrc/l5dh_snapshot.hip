@@ -151,7 +151,15 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
       }
       plan.hot_list[xa] = t;
     } else if (c.ci) {
-      plan.cold_tile[ca] = t;
+      uint4 ci = make_uint4(t | (dirty[t] ? CI_DIRTY : 0u), 0u, 0u, 0u);
+      if (segs.n > 0) {  // segment 0's key ranges (the cold kernel prefetches them with one load)
+        const KeyRange r0 = seg_key(segs, 0, F, t, 0), r1 = seg_key(segs, 0, F, t, 1);
+        ci.x |= r0.r32 ? CI_R32 : 0u;
+        ci.y = r0.a;
+        ci.z = r1.a;
+        ci.w = (r0.e - r0.a) | ((r1.e - r1.a) << 16);
+      }
+      plan.cold_item[ca] = ci;
     }
     plan.tile_flags[t] = flags;
   }
@@ -374,53 +382,59 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
     for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
   }
-  // the next item, fetched during this item's emission (its latency hides behind the
-  // dense stores): tile, dirty flag, sumfix entry, and -- one pending segment, the
-  // common case -- both halves' key ranges and each thread's first 16-B group of them
+  // The next item is fetched during this item's emission (its latency hides behind the
+  // dense stores), from its cold-item entry loaded one item earlier: sumfix and -- one
+  // pending segment, the common case -- each thread's first 16-B group of both halves.
+  // Every load is unconditional (clamped indices, masked where used), so no wait for
+  // it is placed before the emission.
   const bool one = segs.n == 1;
-  uint32_t t = 0;
-  bool dirty = false;
-  int64_t f = 0;
-  KeyRange q0{}, q1{};
+  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0;
+  bool dirty = false, r32 = false;
+  int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
-  auto fetch = [&](uint32_t it) {
-    if (it >= cold_items) return;
-    t = plan.cold_tile[it];
-    dirty = (plan.tile_flags[t] & TF_DIRTY) != 0;
-    if (threadIdx.x < TILE) {
-      const uint32_t s = t * TILE + threadIdx.x;
-      f = 0;
-      if (s < st.S) {
-        f = st.sumfix[s];
-        if (f) st.sumfix[s] = 0;
-      }
-    }
+  const char* const b32 = reinterpret_cast<const char*>(segs.rec32[0]);
+  const char* const b16 = reinterpret_cast<const char*>(segs.rec16[0]);
+  auto fetch = [&](uint4 ci) {
+    // (the entry stays in VGPRs until here, where it becomes scalars: converted at its
+    // load, it would be waited for there)
+    asm volatile("" : "+v"(ci.x), "+v"(ci.y), "+v"(ci.z), "+v"(ci.w));
+    const uint32_t cx = __builtin_amdgcn_readfirstlane(ci.x), cw = __builtin_amdgcn_readfirstlane(ci.w);
+    t = cx & 0x7FFFu;
+    dirty = (cx & CI_DIRTY) != 0u;
+    r32 = (cx & CI_R32) != 0u;
+    a0 = __builtin_amdgcn_readfirstlane(ci.y);
+    a1 = __builtin_amdgcn_readfirstlane(ci.z);
+    n0 = cw & 0xFFFFu;
+    n1 = cw >> 16;
     if (one) {
-      q0 = seg_key(segs, 0, F, t, 0);
-      q1 = seg_key(segs, 0, F, t, 1);
       const uint32_t g = threadIdx.x;
-      if (q0.r32) {
-        x0 = 4 * g < q0.e - q0.a ? reinterpret_cast<const uint4*>(q0.r32 + q0.a)[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
-        x1 = 4 * g < q1.e - q1.a ? reinterpret_cast<const uint4*>(q1.r32 + q1.a)[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
-      } else {
-        x0 = 8 * g < q0.e - q0.a ? reinterpret_cast<const uint4*>(q0.r16 + q0.a)[g] : make_uint4(0u, 0u, 0u, 0u);
-        x1 = 8 * g < q1.e - q1.a ? reinterpret_cast<const uint4*>(q1.r16 + q1.a)[g] : make_uint4(0u, 0u, 0u, 0u);
-      }
+      const uint32_t per = r32 ? 4u : 8u, esz = r32 ? 4u : 2u;
+      const char* base = r32 ? b32 : b16;
+      x0 = *reinterpret_cast<const uint4*>(base + (size_t)esz * (per * g < n0 ? a0 + per * g : a0));
+      x1 = *reinterpret_cast<const uint4*>(base + (size_t)esz * (per * g < n1 ? a1 + per * g : a1));
     }
+    fraw = st.sumfix[min(t * TILE + (threadIdx.x & (TILE - 1)), st.S - 1)];
   };
-  fetch(blockIdx.x);
+  const uint4* __restrict__ citem = plan.cold_item;
+  const uint32_t last = cold_items - 1u;
+  if (blockIdx.x < cold_items) fetch(citem[blockIdx.x]);
+  uint4 cn = citem[min(blockIdx.x + gridDim.x, last)];  // the next item's entry, in flight
   __syncthreads();
   for (uint32_t item = blockIdx.x; item < cold_items; item += gridDim.x) {
     const uint32_t tc = t;
     const bool dc = dirty;
-    if (threadIdx.x < TILE) fixl[threadIdx.x] = f;
+    if (threadIdx.x < TILE) {
+      const uint32_t s = tc * TILE + threadIdx.x;
+      const int64_t f = s < st.S ? fraw : 0;
+      fixl[threadIdx.x] = f;
+      if (f) st.sumfix[s] = 0;
+    }
     if (one) {
       // group g of both halves: the prefetched first one, then g + NT, ...
-      const uint32_t n0 = q0.e - q0.a, n1 = q1.e - q1.a;
-      if (q0.r32) {
+      if (r32) {
         const uint32_t g0 = (n0 + 3) / 4, g1 = (n1 + 3) / 4, gm = max(g0, g1);
-        const uint4* p0 = reinterpret_cast<const uint4*>(q0.r32 + q0.a);
-        const uint4* p1 = reinterpret_cast<const uint4*>(q1.r32 + q1.a);
+        const uint4* p0 = reinterpret_cast<const uint4*>(segs.rec32[0] + a0);
+        const uint4* p1 = reinterpret_cast<const uint4*>(segs.rec32[0] + a1);
         uint4 x = x0, y = x1;
         for (uint32_t g = threadIdx.x; g < gm; g += NT) {
           uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
@@ -436,8 +450,8 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
         }
       } else {
         const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
-        const uint4* p0 = reinterpret_cast<const uint4*>(q0.r16 + q0.a);
-        const uint4* p1 = reinterpret_cast<const uint4*>(q1.r16 + q1.a);
+        const uint4* p0 = reinterpret_cast<const uint4*>(segs.rec16[0] + a0);
+        const uint4* p1 = reinterpret_cast<const uint4*>(segs.rec16[0] + a1);
         uint4 x = x0, y = x1;
         for (uint32_t g = threadIdx.x; g < gm; g += NT) {
           const uint4 cx = x, cy = y;
@@ -452,7 +466,8 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
       count_tile<NT>(segs, F, tc, lut2, hist_add, sum_add);
     }
     __syncthreads();  // counts complete; fixl visible
-    fetch(item + gridDim.x);
+    fetch(cn);  // (past the last item: a harmless refetch of the last entry)
+    cn = citem[min(item + 2u * gridDim.x, last)];
     const uint32_t s0 = tc * TILE;
     // linear emission: a clean whole tile inside the output range of a resetting
     // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
