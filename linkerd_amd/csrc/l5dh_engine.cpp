@@ -514,6 +514,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + the trash bin
   a.pct = c->region_pct;
   a.vec = vec;
+  a.l1 = (int)((c->variant >> 2) & 3u);  // variant bits 3:2: the level-1 kernel (A/B timing)
   {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_ingest(a, 0, c->stream));
@@ -1284,7 +1285,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       return 0;
     }
     case L5DH_PARAM_VARIANT:
-      if (v < 0 || v > 3) return fail(c, -EINVAL, "variant bits must be in [0, 3]");
+      if (v < 0 || v > 15) return fail(c, -EINVAL, "variant bits must be in [0, 15]");
       c->variant = (uint32_t)v;
       return 0;
     case L5DH_PARAM_REGION_PCT:

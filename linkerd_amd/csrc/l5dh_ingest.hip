@@ -464,6 +464,249 @@ __global__ __launch_bounds__(NT, 1) void k_rbin1(const uint32_t* __restrict__ se
 }
 
 // ------------------------------------------------------------------------
+// Level 1 with 24K-slot sub-chunks (1.5x k_rbin1's, so runs 1.5x as long): the stage
+// holds records only (4 B), and each entry's bin is recovered at write-out from a run
+// head bitmap -- bit off[b] set for every non-empty bin b -- as the number of heads at
+// or before the entry: a per-64-entry group prefix (gpre) plus a popcount of the
+// group's 64 bits, indexing the runs' destination deltas (rdelta[run] = run base -
+// stage offset, or INVALID).  Same bins, ranking, reservations and redo as k_rbin1.
+// LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
+// rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2.
+constexpr int CHW = 24576;
+constexpr size_t rbin1w_lds() { return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + 16; }
+
+template <int NT>
+__global__ __launch_bounds__(NT, 1) void k_rbin1w(const uint32_t* __restrict__ series, const float* __restrict__ values,
+                                                  size_t n, size_t per, uint32_t S, uint32_t F, Tables tb,
+                                                  uint32_t* __restrict__ meta, uint32_t* __restrict__ rec32,
+                                                  int64_t* __restrict__ sumfix, uint32_t* __restrict__ err, int vec,
+                                                  int pass) {
+  constexpr int CH = CHW;
+  constexpr int PT = CH / NT;  // slots per thread, loaded and ranked in halves
+  constexpr int PH = PT / 2;
+  static_assert(PH % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* stage = smem;                                        // [CH] records, sorted by bin
+  uint32_t* cnt = stage + CH;                                    // [BIN1_BINS]
+  uint32_t* offr = cnt + BIN1_BINS;                              // [BIN1_BINS] stage offset | run rank << 16
+  uint32_t* rdelta = offr + BIN1_BINS;                           // [BIN1_BINS] by run rank
+  uint32_t* heads = rdelta + BIN1_BINS;                          // [CH / 32] run heads
+  uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
+  uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
+  __shared__ uint32_t nruns;
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
+  uint32_t* bcnt = meta + L.bcnt();
+  const uint32_t* bbase = meta + L.bbase();
+  const uint32_t* bcap = meta + L.bcap();
+  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
+  const uint32_t NW = (F + 31) / 32;
+  const uint32_t ND = hdr[H_ND];
+  const uint32_t TB = FS + 2 * ND;
+  const bool hotrank = hdr[H_HS] != 0u;
+  const uint32_t hb0 = hdr[H_HB0], hb1 = hdr[H_HB1];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const unsigned long long mle = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
+  for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(meta[L.dbits() + w], meta[L.dpre() + w]);
+  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) cnt[b] = 0;
+  __syncthreads();
+  // (a batch piece holds < 2^30 samples: 32-bit sample indices)
+  const uint32_t lo = (uint32_t)((size_t)blockIdx.x * per);
+  const uint32_t hi = (uint32_t)min((size_t)lo + per, n);
+  bool bad = false;
+  for (uint32_t c0 = lo; c0 < hi; c0 += CH) {
+    for (uint32_t wd = threadIdx.x; wd < CH / 32; wd += NT) heads[wd] = 0u;
+    uint32_t rec[PT];
+    uint32_t pk[PT];  // [14:0] rank | [24:15] bin
+    const bool full = vec && c0 + (uint32_t)CH <= hi;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t sv[PH];
+      float fv[PH];
+      if (full) {
+#pragma unroll
+        for (int k = 0; k < PH / 4; ++k) {
+          const uint32_t base = c0 + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
+          const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
+          const float4 f4 = *reinterpret_cast<const float4*>(values + base);
+          sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
+          fv[4 * k] = f4.x; fv[4 * k + 1] = f4.y; fv[4 * k + 2] = f4.z; fv[4 * k + 3] = f4.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < PH; ++k) {
+          const uint32_t i = c0 + 4u * ((uint32_t)(h * (PH / 4) + (k >> 2)) * NT + threadIdx.x) + (uint32_t)(k & 3);
+          const bool in = i < hi;
+          sv[k] = in ? series[i] : 0xFFFFFFFFu;
+          fv[k] = in ? values[i] : 0.0f;
+          bad |= in && sv[k] >= S;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < PH; g += 4) {
+        uint32_t pl[4];
+        uint32_t escm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float f = fv[g + q];
+          const bool fast = __float_as_uint(f) < 0x49FFC000u;  // bits of (float)V_ESC
+          pl[q] = fast ? (uint32_t)f : 0u;
+          escm |= (!fast && sv[g + q] < S) ? (1u << q) : 0u;
+          if (full) bad |= sv[g + q] >= S;
+        }
+        if (__ballot(escm != 0u)) {
+          uint32_t* tmp = stage + threadIdx.x * 8;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            tmp[2 * q] = sv[g + q];
+            tmp[2 * q + 1] = __float_as_uint(fv[g + q]);
+          }
+#pragma unroll 1
+          for (int q = 0; q < 4; ++q)
+            if ((escm >> q) & 1u)
+              tmp[2 * q] = pass == 0 ? payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix)
+                                     : payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, nullptr);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if ((escm >> q) & 1u) pl[q] = tmp[2 * q];
+        }
+        uint2 dv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
+        uint32_t bn[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t s = sv[g + q];
+          const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);
+          const bool direct = __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
+          rec[h * PH + g + q] = ((s & (ST_TILES * TILE - 1)) << 21) | pl[q];
+          const uint32_t dbin =
+              FS + 2u * (dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw))) + ((s >> 4) & 1u);
+          bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+        }
+        if (!hotrank) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pk[h * PH + g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 15);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pk[h * PH + g + q] = bn[q] << 15;
+        }
+        asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
+      }
+    }
+    if (hotrank) {
+      uint32_t wc0 = 0, wc1 = 0;
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint32_t b = pk[k] >> 15;
+        const bool m0 = b == hb0, m1 = b == hb1;
+        wc0 += (uint32_t)__popcll(__ballot(m0));
+        wc1 += (uint32_t)__popcll(__ballot(m1));
+        if (!m0 && !m1) pk[k] |= atomicAdd(cnt + b, 1u);
+      }
+      uint32_t base = 0;
+      if (lane == 0 && wc0) base = atomicAdd(cnt + hb0, wc0);
+      if (lane == 1 && wc1) base = atomicAdd(cnt + hb1, wc1);
+      uint32_t r0 = __builtin_amdgcn_readlane(base, 0), r1 = __builtin_amdgcn_readlane(base, 1);
+#pragma unroll
+      for (int k = 0; k < PT; ++k) {
+        const uint32_t b = pk[k] >> 15;
+        const bool m0 = b == hb0, m1 = b == hb1;
+        const unsigned long long x0 = __ballot(m0), x1 = __ballot(m1);
+        if (m0) pk[k] |= r0 + mask_below(x0);
+        if (m1) pk[k] |= r1 + mask_below(x1);
+        r0 += (uint32_t)__popcll(x0);
+        r1 += (uint32_t)__popcll(x1);
+      }
+    }
+    __syncthreads();  // B1: counts complete
+    // run reservations: thread t -> bins t, t + NT, ... (the trash bin TB gets none)
+    constexpr int RB = (BIN1_BINS + NT - 1) / NT;
+    uint32_t rn[RB], rold[RB], rbase[RB], rcapv[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
+      rn[j] = rb_bin <= TB ? cnt[rb_bin] : 0u;  // records of the bin in this sub-chunk
+      rold[j] = rbase[j] = rcapv[j] = 0;
+      if (rb_bin < TB && rn[j]) {
+        rold[j] = atomicAdd(&bcnt[rb_bin], rn[j]);
+        rbase[j] = bbase[rb_bin];
+        rcapv[j] = bcap[rb_bin];
+      }
+    }
+    if (wv == 0) {  // one wave: stage offsets and run ranks (DPP scans of 16 bins per lane), run heads
+      uint32_t c[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cnt + 16 * lane + 4 * q);
+        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+      }
+      uint32_t tl = 0, tr = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        tl += c[q];
+        tr += c[q] ? 1u : 0u;
+      }
+      uint32_t e = wave_incl_scan32(tl) - tl;
+      const uint32_t rin = wave_incl_scan32(tr);
+      uint32_t r = rin - tr;
+      if (lane == 63) nruns = rin;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        offr[16 * lane + q] = e | (r << 16);
+        if (c[q]) atomicOr(&heads[e >> 5], 1u << (e & 31u));
+        e += c[q];
+        r += c[q] ? 1u : 0u;
+      }
+    }
+    __syncthreads();  // B2: offsets, run ranks, heads
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t bin = pk[k] >> 15;
+      stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
+    }
+    if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
+      const uint32_t at = threadIdx.x * 64u;
+      uint32_t lb = 0, hb = BIN1_BINS;  // first b with offset(b) >= at
+      while (lb < hb) {
+        const uint32_t m = (lb + hb) >> 1;
+        if ((offr[m] & 0xFFFFu) < at) lb = m + 1; else hb = m;
+      }
+      gpre[threadIdx.x] = (uint16_t)(lb < BIN1_BINS ? offr[lb] >> 16 : nruns);
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
+      if (rn[j]) {
+        uint32_t d = INVALID;
+        if (rb_bin < TB) {
+          if (rold[j] + rn[j] <= rcapv[j]) d = rbase[j] + rold[j] - (offr[rb_bin] & 0xFFFFu);
+          else hdr[H_OV1] = 1u;  // this run is dropped; k_rfix1 has the batch redone with exact regions
+        }
+        rdelta[offr[rb_bin] >> 16] = d;
+      }
+    }
+    __syncthreads();  // B3: stage, group prefixes, deltas (every count read: cleared below)
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+      if (threadIdx.x + (uint32_t)j * NT < BIN1_BINS) cnt[threadIdx.x + (uint32_t)j * NT] = 0;
+#pragma unroll 4
+    for (int k = 0; k < PT; ++k) {  // all CH entries, in sorted order (each wave a contiguous PT x 64 range)
+      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
+      const uint32_t g = i >> 6;  // (wave-uniform)
+      const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
+      const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
+      const uint32_t d = rdelta[run];
+      if (d != INVALID) rec32[i + d] = stage[i];
+    }
+    __syncthreads();  // B4
+  }
+  if (pass == 0 && bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
+}
+
+// ------------------------------------------------------------------------
 // After level 1 (one workgroup, thread = bin): exact bin totals, the direct keys'
 // ranges, and on an overflow exact regions for the redo pass.
 __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict__ meta, const uint32_t* __restrict__ err,
@@ -871,6 +1114,13 @@ hipError_t set_ingest_attributes() {
   if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rbin1_lds(CH1))))
     return e;
+  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds())) ||
+      (e = hipFuncSetAttribute((const void*)k_rbin1w<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds())) ||
+      (e = hipFuncSetAttribute((const void*)k_rbin1w<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds())))
+    return e;
   return hipFuncSetAttribute((const void*)k_rbin2<B2_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
 }
 
@@ -885,8 +1135,23 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
       break;
     case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
       for (int pass = 0; pass < 2; ++pass) {
-        hipLaunchKernelGGL((k_rbin1<CH1, 1024>), dim3(a.G), dim3(1024), rbin1_lds(CH1), st, a.series, a.values, a.n,
-                           a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+        switch (a.l1) {
+          case 1:
+            hipLaunchKernelGGL((k_rbin1<CH1, 1024>), dim3(a.G), dim3(1024), rbin1_lds(CH1), st, a.series, a.values,
+                               a.n, a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+            break;
+          case 2:
+            hipLaunchKernelGGL((k_rbin1w<512>), dim3(a.G), dim3(512), rbin1w_lds(), st, a.series, a.values, a.n,
+                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+            break;
+          case 3:
+            hipLaunchKernelGGL((k_rbin1w<1024>), dim3(a.G), dim3(1024), rbin1w_lds(), st, a.series, a.values, a.n,
+                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+            break;
+          default:
+            hipLaunchKernelGGL((k_rbin1w<768>), dim3(a.G), dim3(768), rbin1w_lds(), st, a.series, a.values, a.n,
+                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+        }
         if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);
       }
       break;
