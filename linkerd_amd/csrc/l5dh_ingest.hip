@@ -473,15 +473,14 @@ __global__ __launch_bounds__(NT, 1) void k_rbin1(const uint32_t* __restrict__ se
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2.
 constexpr int CHW = 24576;
-constexpr size_t rbin1w_lds() { return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + 16; }
+constexpr size_t rbin1w_lds(int ch) { return (size_t)ch * 4 + BIN1_BINS * 12 + ch / 8 + ch / 32 + 1024 * 8 + 16; }
 
-template <int NT>
-__global__ __launch_bounds__(NT, 1) void k_rbin1w(const uint32_t* __restrict__ series, const float* __restrict__ values,
+template <int NT, int CH>
+__global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                   size_t n, size_t per, uint32_t S, uint32_t F, Tables tb,
                                                   uint32_t* __restrict__ meta, uint32_t* __restrict__ rec32,
                                                   int64_t* __restrict__ sumfix, uint32_t* __restrict__ err, int vec,
                                                   int pass) {
-  constexpr int CH = CHW;
   constexpr int PT = CH / NT;  // slots per thread, loaded and ranked in halves
   constexpr int PH = PT / 2;
   static_assert(PH % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
@@ -699,7 +698,11 @@ __global__ __launch_bounds__(NT, 1) void k_rbin1w(const uint32_t* __restrict__ s
       const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
+#if defined(L5DH_EXP) && (L5DH_EXP & 32)  // timing only: the same records written sequentially
+      if (d != INVALID) rec32[c0 + i] = stage[i];
+#else
       if (d != INVALID) rec32[i + d] = stage[i];
+#endif
     }
     __syncthreads();  // B4
   }
@@ -1114,12 +1117,12 @@ hipError_t set_ingest_attributes() {
   if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rbin1_lds(CH1))))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<768>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds())) ||
-      (e = hipFuncSetAttribute((const void*)k_rbin1w<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds())) ||
-      (e = hipFuncSetAttribute((const void*)k_rbin1w<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds())))
+  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<768, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds(CHW))) ||
+      (e = hipFuncSetAttribute((const void*)k_rbin1w<512, 8192>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds(8192))) ||
+      (e = hipFuncSetAttribute((const void*)k_rbin1w<1024, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds(CHW))))
     return e;
   return hipFuncSetAttribute((const void*)k_rbin2<B2_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
 }
@@ -1140,16 +1143,21 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
             hipLaunchKernelGGL((k_rbin1<CH1, 1024>), dim3(a.G), dim3(1024), rbin1_lds(CH1), st, a.series, a.values,
                                a.n, a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
             break;
-          case 2:
-            hipLaunchKernelGGL((k_rbin1w<512>), dim3(a.G), dim3(512), rbin1w_lds(), st, a.series, a.values, a.n,
-                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+          case 2: {  // 8K-slot sub-chunks, two 512-thread workgroups per CU (twice the slabs)
+            const size_t G2 = std::min<size_t>(2 * (size_t)a.G, (a.n + 8191) / 8192);
+            size_t per2 = ((a.n + G2 - 1) / G2 + 3) & ~(size_t)3;
+            const size_t g2 = (a.n + per2 - 1) / per2;
+            hipLaunchKernelGGL((k_rbin1w<512, 8192>), dim3((unsigned)std::max<size_t>(g2, 1)), dim3(512),
+                               rbin1w_lds(8192), st, a.series, a.values, a.n, per2, a.S, a.F, a.tb, a.meta, a.rec32,
+                               a.sumfix, a.err, a.vec ? 1 : 0, pass);
             break;
+          }
           case 3:
-            hipLaunchKernelGGL((k_rbin1w<1024>), dim3(a.G), dim3(1024), rbin1w_lds(), st, a.series, a.values, a.n,
-                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
+            hipLaunchKernelGGL((k_rbin1w<1024, CHW>), dim3(a.G), dim3(1024), rbin1w_lds(CHW), st, a.series, a.values,
+                               a.n, a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
             break;
           default:
-            hipLaunchKernelGGL((k_rbin1w<768>), dim3(a.G), dim3(768), rbin1w_lds(), st, a.series, a.values, a.n,
+            hipLaunchKernelGGL((k_rbin1w<768, CHW>), dim3(a.G), dim3(768), rbin1w_lds(CHW), st, a.series, a.values, a.n,
                                a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
         }
         if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);

@@ -160,7 +160,7 @@ struct IngestArgs {
   uint32_t pct;            // region capacity scale, percent (100: as predicted)
   bool vec;                // 16-B aligned inputs
   int l1;                  // level-1 kernel: 0 k_rbin1w<768> (24K-slot sub-chunks), 1 k_rbin1 (16K),
-                           // 2 k_rbin1w<512>, 3 k_rbin1w<1024> (L5DH_PARAM_VARIANT bits 3:2)
+                           // 2 k_rbin1w<512> (8K slots, 2 per CU), 3 k_rbin1w<1024> (L5DH_PARAM_VARIANT bits 3:2)
 };
 // Stages: 0 = sample + level-1 plan + level 1 (+ redo), 1 = level-2 plan + level 2 (+ redo).
 hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st);
