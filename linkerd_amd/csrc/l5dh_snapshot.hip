@@ -688,11 +688,12 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       if (lo >= hi) continue;
       // [a, e) of this range; hot_chunk is a multiple of 1024, so a chunk starts 16-B aligned
       const uint32_t a = r.a + (uint32_t)skip, e = a + (uint32_t)(hi - lo);
+      // loads are unconditional (a group past the range reloads the first one; records
+      // outside [a, e) are masked where they are used), so the next groups stay in flight
+      // while this one is counted
       if (r.r32) {
         const uint32_t a4 = a & ~3u;
-        auto ld = [&](uint32_t g) {
-          return g < e ? *reinterpret_cast<const uint4*>(r.r32 + g) : make_uint4(0u, 0u, 0u, 0u);
-        };
+        auto ld = [&](uint32_t g) { return *reinterpret_cast<const uint4*>(r.r32 + (g < e ? g : a4)); };
         uint32_t g = a4 + 4u * threadIdx.x;
         uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
         for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
@@ -709,9 +710,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
         }
       } else {
         const uint32_t a8 = a & ~7u;
-        auto ld = [&](uint32_t g) {
-          return g < e ? *reinterpret_cast<const uint4*>(r.r16 + g) : make_uint4(0u, 0u, 0u, 0u);
-        };
+        auto ld = [&](uint32_t g) { return *reinterpret_cast<const uint4*>(r.r16 + (g < e ? g : a8)); };
         uint32_t g = a8 + 8u * threadIdx.x;
         uint4 n0 = ld(g), n1 = ld(g + 8u * WG);
         for (uint32_t c = a8; c < e; c += 16u * WG, g += 16u * WG) {
