@@ -588,41 +588,39 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
     __syncthreads();
     const size_t lo = item * chunk, hi = lo + chunk < n ? lo + chunk : n;
     if (vec) {  // 16-B loads (lo is a multiple of chunk, itself of 4); one group ahead in flight
-      auto ld = [&](size_t g, uint4& sv, uint4& vv) {
-        sv = vv = make_uint4(0u, 0u, 0u, 0u);
-        if (g + 4 <= hi) {
-          sv = *reinterpret_cast<const uint4*>(series + g);
-          vv = *reinterpret_cast<const uint4*>(values + g);
-        } else if (g < hi) {  // the batch's ragged end
-          sv.x = series[g];
-          vv.x = __float_as_uint(values[g]);
-          if (g + 1 < hi) {
-            sv.y = series[g + 1];
-            vv.y = __float_as_uint(values[g + 1]);
-          }
-          if (g + 2 < hi) {
-            sv.z = series[g + 2];
-            vv.z = __float_as_uint(values[g + 2]);
-          }
-        }
-      };
-      size_t g = lo + 4u * threadIdx.x;
-      uint4 s0, v0, s1, v1;
-      ld(g, s0, v0);
-      ld(g + 4u * WG, s1, v1);
-      for (size_t c = lo; c < hi; c += 8u * WG, g += 8u * WG) {
-        const uint4 cs0 = s0, cv0 = v0, cs1 = s1, cv1 = v1;
-        ld(g + 8u * WG, s0, v0);
-        ld(g + 12u * WG, s1, v1);
-        const uint32_t ss[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
-        const uint32_t vv[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
-        uint32_t x[8];
+      // whole groups [lo, hi4) with unconditional loads (a group past the end reloads the
+      // last whole one; masked where used), so the next groups stay in flight; then the
+      // batch's ragged end, at most 3 samples
+      const size_t hi4 = lo + ((hi - lo) & ~(size_t)3);
+      if (hi4 > lo) {
+        auto ld = [&](size_t g, uint4& sv, uint4& vv) {
+          const size_t gc = g < hi4 ? g : hi4 - 4;
+          sv = *reinterpret_cast<const uint4*>(series + gc);
+          vv = *reinterpret_cast<const uint4*>(values + gc);
+        };
+        size_t g = lo + 4u * threadIdx.x;
+        uint4 s0, v0, s1, v1;
+        ld(g, s0, v0);
+        ld(g + 4u * WG, s1, v1);
+        for (size_t c = lo; c < hi4; c += 8u * WG, g += 8u * WG) {
+          const uint4 cs0 = s0, cv0 = v0, cs1 = s1, cv1 = v1;
+          ld(g + 8u * WG, s0, v0);
+          ld(g + 12u * WG, s1, v1);
+          const uint32_t ss[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
+          const uint32_t vv[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+          uint32_t x[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const size_t gk = g + (k >> 2) * 4u * WG + (k & 3);
-          x[k] = gk < hi ? enc(ss[k], __uint_as_float(vv[k])) : 0xFFFFFFFFu;
+          for (int k = 0; k < 8; ++k) {
+            const size_t gk = g + (k >> 2) * 4u * WG + (k & 3);
+            x[k] = gk < hi4 ? enc(ss[k], __uint_as_float(vv[k])) : 0xFFFFFFFFu;
+          }
+          count_batch<8>(x, lut2, hist_add, sum_add);
         }
-        count_batch<8>(x, lut2, hist_add, sum_add);
+      }
+      if (threadIdx.x < hi - hi4) {
+        const size_t g = hi4 + threadIdx.x;
+        const uint32_t x[1] = {enc(series[g], values[g])};
+        count_batch<1>(x, lut2, hist_add, sum_add);
       }
     } else {
       for (size_t g = lo + threadIdx.x; g < hi; g += WG) {
