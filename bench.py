@@ -280,7 +280,7 @@ def load_pmc_traffic(path, pl):
         return {}, "PMC summary is of another workload"
     if pm.get("src_hash") != engine_source_hash():
         return {}, "stale: PMC summary measured other engine sources (re-run tools/profile_pmc.sh)"
-    parts = {"count": ["count"], "bin1": ["bin1"], "bin2": ["bin2"], "accum": ["accum_cold_p", "accum_split"]}
+    parts = {"bin1": ["rbin1w"], "bin2": ["rbin2"], "accum": ["accum_cold_p", "accum_split"]}
     ks = pm.get("kernels", {})
     out = {name: int(sum(ks[p]["hbm_bytes_per_launch"] for p in ps)) for name, ps in parts.items()
            if all(p in ks and "hbm_bytes_per_launch" in ks[p] for p in ps)}

@@ -28,7 +28,14 @@ def main(d, out_json=None, meta=None):
         # steady state: the first dispatch of a kernel runs before the engine has
         # a split set (the previous batch's big tiles), so it is dropped when
         # there are >= 3 dispatches
-        row = {c: (sum(v[1:]) / (len(v) - 1) if len(v) >= 3 else sum(v) / len(v)) for c, v in cs.items()}
+        # dispatches that did (almost) nothing -- a redo pass that exits at once -- are
+        # not launches of the work being measured: drop those under 2 % of the max
+        def steady(v):
+            v = v[1:] if len(v) >= 3 else v
+            top = max(v) if v else 0.0
+            w = [x for x in v if x >= 0.02 * top] or v
+            return sum(w) / len(w)
+        row = {c: steady(v) for c, v in cs.items()}
         if "FETCH_SIZE" in row or "WRITE_SIZE" in row:
             rd = 2 * 1024 * row.get("FETCH_SIZE", 0.0)
             wr = 1024 * row.get("WRITE_SIZE", 0.0)
