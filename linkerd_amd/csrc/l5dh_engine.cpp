@@ -409,12 +409,12 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     if (split_items) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) == 0, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) == 0, c->stream));
     }
   }
   if (hot) {
@@ -1285,7 +1285,7 @@ int l5dh_set_param(l5dh_ctx* c, int param, int64_t v) {
       return 0;
     }
     case L5DH_PARAM_VARIANT:
-      if (v < 0 || v > 15) return fail(c, -EINVAL, "variant bits must be in [0, 15]");
+      if (v < 0 || v > 31) return fail(c, -EINVAL, "variant bits must be in [0, 31]");
       c->variant = (uint32_t)v;
       return 0;
     case L5DH_PARAM_REGION_PCT:

@@ -184,7 +184,7 @@ constexpr uint32_t DEV_COUNT = 0xFFFFFFFFu;
 // instead of their state rows, and k_hot_finish summarizes them in place.
 hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, hipStream_t st);
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
-                             int final_mode, int reset, hipStream_t st);
+                             int final_mode, int reset, int stores_first, hipStream_t st);
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
                               Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,

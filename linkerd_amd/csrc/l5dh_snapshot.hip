@@ -356,7 +356,8 @@ __device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t 
 // wave per series emits the dense row and the summary.  The LUT and the midpoints
 // are staged once; each wave clears its series' LDS rows right after emitting them.
 __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                          uint32_t cold_arg, int final_mode, int reset) {
+                                                          uint32_t cold_arg, int final_mode, int reset,
+                                                          int stores_first) {
   constexpr int NT = 1024;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t cold_items = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
@@ -476,6 +477,29 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
                         s0 + TILE <= st.S && (oi0 & 1u) == 0u;
+    // linear: the 32 rows' stores are issued first (chunk c = flat elements 4c..4c+3 of
+    // [32][1798]: two u16 pairs), the summaries are computed while they drain, and the
+    // rows are cleared once both have read them (stores_first = 0: summaries, then the
+    // stores, each clearing the words it read -- the round-2 order, for A/B)
+    auto linear_stores = [&](bool clear) {
+      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
+      constexpr int NCH = TILE * NB / 4;
+      for (int c = threadIdx.x; c < NCH; c += NT) {
+        const int e0 = 4 * c;
+        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
+        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
+        // the second pair is the next word (one ds_read2), except for the chunk that
+        // straddles into the next row (b0 = 1796; word 899 of a row is never written)
+        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
+        const uint32_t x = *p0, y = *p1;
+        if (clear) {
+          *p0 = 0u;
+          *p1 = 0u;
+        }
+        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+      }
+    };
+    if (linear && stores_first) linear_stores(false);
     for (int loc = w; loc < TILE; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
@@ -499,22 +523,12 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
       vsl[loc * 64 + lane] = 0u;
     }
     if (linear) {
-      __syncthreads();  // summaries have read the rows
-      // chunk c = flat elements 4c..4c+3 of [32][1798]: two u16 pairs, each an LDS word
-      // read by this chunk only (and cleared here; word 899 of a row is never written)
-      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
-      constexpr int NCH = TILE * NB / 4;
-      for (int c = threadIdx.x; c < NCH; c += NT) {
-        const int e0 = 4 * c;
-        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
-        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
-        // the second pair is the next word (one ds_read2/ds_write2), except for the
-        // chunk that straddles into the next row (b0 = 1796)
-        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
-        const uint32_t x = *p0, y = *p1;
-        *p0 = 0u;
-        *p1 = 0u;
-        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+      __syncthreads();  // the stores and the summaries have read the rows
+      if (stores_first) {
+        uint4* hp = reinterpret_cast<uint4*>(hist);
+        for (int i = threadIdx.x; i < TILE * CROW / 4; i += NT) hp[i] = make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        linear_stores(true);
       }
     }
     if (threadIdx.x == 0) st.dirty[tc] = keep ? 1 : 0;
@@ -896,13 +910,13 @@ hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out
 }
 
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
-                             int final_mode, int reset, hipStream_t st) {
+                             int final_mode, int reset, int stores_first, hipStream_t st) {
   if (cold_items == 0) return hipSuccess;
   // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
   // may be DEV_COUNT (read on the device)
   const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
   hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan, state, tb, out,
-                     cold_items, final_mode, reset);
+                     cold_items, final_mode, reset, stores_first);
   return hipGetLastError();
 }
 
