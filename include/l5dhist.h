@@ -79,7 +79,7 @@ enum {
                                   every variant computes the same results; bit 0: one-tile folds in u16 bins;
                                   bit 1: DMA copies of pinned host batches; bits 3:2: level-1 kernel (1: 16K-slot
                                   sub-chunks, 2: 8K-slot sub-chunks two workgroups per CU); bit 4: cold tiles'
-                                  summaries before their dense stores) */
+                                  dense stores before their summaries) */
 };
 
 /* Fleet-merge modes for l5dh_merge */

@@ -208,6 +208,26 @@ __device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& 
 
 constexpr int NB4 = 450;  // groups of 4 bins covering 1798 bins (+2 padding)
 
+// The fleet merge's encoding words of one row (non-empty buckets, + 1 per count >=
+// MERGE_CMAX), written by lane 0 to *out when out is non-null.  One wave.
+template <class Src>
+__device__ __forceinline__ void row_words(const Src& src, uint32_t* __restrict__ out) {
+  if (out == nullptr) return;
+  const int lane = lane_id();
+  const int ng = lane_groups(lane);
+  uint32_t w = 0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    if (q < ng) {
+      const uint4 v = src.get4(28 * lane + 4 * q);
+      w += (v.x != 0u) + (v.y != 0u) + (v.z != 0u) + (v.w != 0u);
+      w += (v.x >= MERGE_CMAX) + (v.y >= MERGE_CMAX) + (v.z >= MERGE_CMAX) + (v.w >= MERGE_CMAX);
+    }
+  }
+  w = (uint32_t)wave_sum((uint64_t)w);
+  if (lane == 0) *out = w;
+}
+
 // Pass over a row source: optional dense copy in a coalesced lane order (lane l
 // copies groups l, l+64, ...), then the blocked group sums of the summary.
 template <class Src>

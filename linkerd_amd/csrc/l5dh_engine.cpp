@@ -409,12 +409,12 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     if (split_items) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) == 0, c->side));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) != 0, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) == 0, c->stream));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) != 0, c->stream));
     }
   }
   if (hot) {
@@ -686,13 +686,18 @@ int merge_export(l5dh_ctx* c) {
   if (r) return r;
   const size_t Sp = (size_t)merge_per(c) * c->nranks;
   if ((r = ensure(c, c->merge_counts, Sp * NB * 4)) || (r = ensure(c, c->merge_totals, Sp * 8))) return r;
+  // the encoding's words per row come out of the export itself (every kernel that
+  // emits a row counts its non-empty buckets), so the rows are read once, by k_menc
+  if ((r = ensure(c, c->m_words, (Sp + 1) * 4))) return r;
   int32_t* cnt = static_cast<int32_t*>(c->merge_counts.p);
   int64_t* tot = static_cast<int64_t*>(c->merge_totals.p);
+  uint32_t* words = static_cast<uint32_t*>(c->m_words.p);
   if (Sp > c->S) {
     HIPCHK(c, hipMemsetAsync(cnt + (size_t)c->S * NB, 0, (Sp - c->S) * NB * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(tot + c->S, 0, (Sp - c->S) * 8, c->stream));
   }
-  return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot});
+  HIPCHK(c, hipMemsetAsync(words + c->S, 0, (Sp + 1 - c->S) * 4, c->stream));
+  return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot, words});
 }
 
 // Phase 2 (reduce-scatter): the rows are exchanged sparse (l5dh_merge.hip) -- per
@@ -718,8 +723,7 @@ int merge_encode_step(l5dh_ctx* c) {
     return r;
   uint32_t* words = static_cast<uint32_t*>(c->m_words.p);
   uint64_t* offs = static_cast<uint64_t*>(c->m_offs.p);
-  HIPCHK(c, merge_count(static_cast<const int32_t*>(c->merge_counts.p), Sp, words, offs, c->m_tmp.p, &c->m_tmp_bytes,
-                        c->stream));
+  HIPCHK(c, merge_count(nullptr, Sp, words, offs, c->m_tmp.p, &c->m_tmp_bytes, c->stream));  // (words: the export's)
   std::vector<uint64_t> bnd(W + 1);
   for (int q = 0; q <= W; ++q)
     HIPCHK(c, hipMemcpyAsync(&bnd[q], offs + (size_t)q * per, 8, hipMemcpyDeviceToHost, c->stream));

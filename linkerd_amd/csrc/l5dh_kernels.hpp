@@ -136,7 +136,10 @@ struct Outputs {
   int32_t* counts;         // nullable, [count][1798]
   uint32_t first, count;
   int64_t* totals;         // nullable, [count] exact sums (the fleet-merge export)
+  uint32_t* words;         // nullable, [count] the fleet merge's encoding words per row: non-empty
+                           // buckets + counts >= MERGE_CMAX (which take a second word)
 };
+constexpr uint32_t MERGE_CMAX = 0x1FFFFFu;  // count field of a merge entry; CMAX marks an escaped count
 
 // ---- ingest launchers (l5dh_ingest.hip; all enqueue on `st`) ----
 struct IngestArgs {

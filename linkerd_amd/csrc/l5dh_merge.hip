@@ -21,7 +21,7 @@
 namespace l5dh {
 namespace {
 
-constexpr uint32_t CMAX = 0x1FFFFFu;  // count field; CMAX marks an escaped count
+constexpr uint32_t CMAX = MERGE_CMAX;  // count field; CMAX marks an escaped count
 
 __global__ __launch_bounds__(256) void k_mcount(const int32_t* __restrict__ rows, uint32_t nrows,
                                                 uint32_t* __restrict__ words) {
@@ -210,7 +210,8 @@ hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uin
     *tmp_bytes = scan_tmp_bytes(nrows + 1);
     return hipSuccess;
   }
-  if (nrows) hipLaunchKernelGGL(k_mcount, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, words);
+  // rows == nullptr: words[0..nrows) were written by the export (Outputs::words)
+  if (rows && nrows) hipLaunchKernelGGL(k_mcount, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, words);
   hipError_t e = hipMemsetAsync(words + nrows, 0, 4, st);  // offs[nrows] = the total
   if (e != hipSuccess) return e;
   return exclusive_scan_u32_u64(words, nrows + 1, offs, tmp, st);

@@ -14,9 +14,9 @@ struct MergeSources {  // the encodings of this rank's row slice, one per source
   int n;
 };
 
-// words[r] = entry words of row r (words needs nrows + 1 slots), offs[0..nrows] their
-// exclusive prefix (offs[nrows] = the total).  tmp == nullptr: *tmp_bytes receives the
-// scan's temporary storage size.
+// words[r] = entry words of row r (words needs nrows + 1 slots; rows == nullptr: already
+// there, from the export), offs[0..nrows] their exclusive prefix (offs[nrows] = the
+// total).  tmp == nullptr: *tmp_bytes receives the scan's temporary storage size.
 hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
                        size_t* tmp_bytes, hipStream_t st);
 hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st);

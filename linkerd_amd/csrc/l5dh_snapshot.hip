@@ -271,10 +271,14 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   if (lane == 0 && emit && out.totals) out.totals[oi] = total;
   if (emit) {
     Summary88* so = out.summ ? out.summ + oi : nullptr;
-    if (dirty)
+    uint32_t* wo = out.words ? out.words + oi : nullptr;
+    if (dirty) {
       wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
-    else
+      row_words(SrcRow32{srow}, wo);
+    } else {
       wave_summary(g, lds, total, tb.mid, so);
+      row_words(lds, wo);
+    }
   }
 }
 
@@ -477,10 +481,10 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
                         s0 + TILE <= st.S && (oi0 & 1u) == 0u;
-    // linear: the 32 rows' stores are issued first (chunk c = flat elements 4c..4c+3 of
-    // [32][1798]: two u16 pairs), the summaries are computed while they drain, and the
-    // rows are cleared once both have read them (stores_first = 0: summaries, then the
-    // stores, each clearing the words it read -- the round-2 order, for A/B)
+    // linear: the summaries, then the 32 rows' stores as one range (chunk c = flat
+    // elements 4c..4c+3 of [32][1798]: two u16 pairs), each clearing the words it read.
+    // (stores_first, variant bit 4: the stores issued before the summaries and the rows
+    // cleared after both -- measured slower, accum 2.40 vs 2.28 ms, profiles/r03n_ab_16.log)
     auto linear_stores = [&](bool clear) {
       uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
       constexpr int NCH = TILE * NB / 4;
@@ -511,6 +515,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
 #pragma unroll
           for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(SrcLds16{row}.get4(28 * lane + 4 * q)) : 0u;
           wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          row_words(SrcLds16{row}, out.words ? out.words + (s - out.first) : nullptr);
           if (lane == 0 && out.totals) out.totals[s - out.first] = (int64_t)vsum + fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
@@ -757,6 +762,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
         uint32_t g[9];
         row_pass(src, g, out.counts + (size_t)s * NB);
         wave_summary(g, src, total, tb.mid, out.summ ? out.summ + s : nullptr);
+        row_words(src, out.words ? out.words + s : nullptr);
         if (lane == 0) {
           st.sumfix[s] = 0;
           st.total[s] = total;
@@ -799,14 +805,17 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
         const uint32_t oi = s - out.first;
         if (s >= out.first && oi < out.count) {
           uint32_t g[9];
+          uint32_t* wo = out.words ? out.words + oi : nullptr;
           if (direct_out && !(plan.tile_flags[t] & TF_DIRTY)) {  // counted in the output row itself
             const SrcExt src{out.counts + (size_t)oi * NB};
             row_pass(src, g, nullptr);
             wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+            row_words(src, wo);
           } else {
             const SrcRow32 src{st.counts + (size_t)s * ROW};
             row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
             wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
+            row_words(src, wo);
           }
           if (lane == 0 && out.totals) out.totals[oi] = total;
         }
@@ -845,6 +854,7 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
     const int64_t total = st.total[s];
     row_pass(src, g, orow);
     if (out.summ) wave_summary(g, src, total, tb.mid, out.summ + i);
+    row_words(src, out.words ? out.words + i : nullptr);
     if (totals_out && lane == 0) totals_out[i] = total;
     if (reset) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -866,6 +876,7 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
     }
     if (out.summ) wave_summary(g, SrcRow32{st.counts}, 0, tb.mid, out.summ + i);  // num == 0: no bin is read
     if (totals_out && lane == 0) totals_out[i] = 0;
+    if (out.words && lane == 0) out.words[i] = 0;
   }
 }
 
