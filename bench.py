@@ -448,7 +448,7 @@ def run(args):
     if fleet:
         first, cnt = state["merged"]
         tot = torch.stack([summ[:cnt, 0].sum(), torch.tensor(0, device=dev)])
-        want = pl["N_total"]
+        want = n if args.shard else pl["N_total"]  # (--shard: this rank's samples, merged alone)
     else:
         tot = torch.stack([counts[:S].sum(dtype=torch.int64), summ[:S, 0].sum()])
         want = n

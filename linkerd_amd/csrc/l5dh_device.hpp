@@ -208,41 +208,50 @@ __device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& 
 
 constexpr int NB4 = 450;  // groups of 4 bins covering 1798 bins (+2 padding)
 
-// The fleet merge's encoding words of one row (non-empty buckets, + 1 per count >=
-// MERGE_CMAX), written by lane 0 to *out when out is non-null.  One wave.
-template <class Src>
-__device__ __forceinline__ void row_words(const Src& src, uint32_t* __restrict__ out) {
+// The fleet merge's encoding words of 4 bins (non-empty buckets, + 1 per count >=
+// MERGE_CMAX, which takes a second word).
+__device__ __forceinline__ uint32_t merge_words4(uint4 v) {
+  return (v.x != 0u) + (v.y != 0u) + (v.z != 0u) + (v.w != 0u) + (v.x >= MERGE_CMAX) + (v.y >= MERGE_CMAX) +
+         (v.z >= MERGE_CMAX) + (v.w >= MERGE_CMAX);
+}
+
+// A wave's per-lane word counts -> *out (lane 0), when out is non-null.
+__device__ __forceinline__ void put_words(uint32_t w, uint32_t* __restrict__ out) {
   if (out == nullptr) return;
-  const int lane = lane_id();
-  const int ng = lane_groups(lane);
-  uint32_t w = 0;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    if (q < ng) {
-      const uint4 v = src.get4(28 * lane + 4 * q);
-      w += (v.x != 0u) + (v.y != 0u) + (v.z != 0u) + (v.w != 0u);
-      w += (v.x >= MERGE_CMAX) + (v.y >= MERGE_CMAX) + (v.z >= MERGE_CMAX) + (v.w >= MERGE_CMAX);
-    }
-  }
   w = (uint32_t)wave_sum((uint64_t)w);
-  if (lane == 0) *out = w;
+  if (lane_id() == 0) *out = w;
 }
 
 // Pass over a row source: optional dense copy in a coalesced lane order (lane l
-// copies groups l, l+64, ...), then the blocked group sums of the summary.
+// copies groups l, l+64, ...), then the blocked group sums of the summary; with
+// words_out, the row's merge-encoding words (counted from the values already read).
 template <class Src>
-__device__ __forceinline__ void row_pass(const Src& src, uint32_t (&g)[9], int32_t* __restrict__ out_row) {
+__device__ __forceinline__ void row_pass(const Src& src, uint32_t (&g)[9], int32_t* __restrict__ out_row,
+                                         uint32_t* __restrict__ words_out = nullptr) {
   const int lane = lane_id();
+  uint32_t w = 0;
   if (out_row) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int q = lane + 64 * k;
-      if (q < NB4) store4_1798(out_row, 4 * q, src.get4(4 * q));
+      if (q < NB4) {
+        const uint4 v = src.get4(4 * q);
+        store4_1798(out_row, 4 * q, v);
+        w += merge_words4(v);
+      }
     }
   }
   const int ng = lane_groups(lane);
 #pragma unroll
-  for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(src.get4(28 * lane + 4 * q)) : 0u;
+  for (int q = 0; q < 9; ++q) {
+    g[q] = 0u;
+    if (q < ng) {
+      const uint4 v = src.get4(28 * lane + 4 * q);
+      g[q] = sum4(v);
+      if (!out_row) w += merge_words4(v);
+    }
+  }
+  put_words(w, words_out);
 }
 
 template <int NT = 1024>

@@ -109,11 +109,12 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
       for (int k = 0; k < 3; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
       y[3] = 0u;
       block_excl_scan4<1024>(y, lds4, ty);
-      if (threadIdx.x == 0) {  // header: cold items, big tiles, (unused), split items
+      if (threadIdx.x == 0) {  // header: cold items, big tiles, cold-item counter, split items
         plan.header[0] = ty[0];
         plan.header[1] = ty[1];
         plan.header[2] = 0u;
         plan.header[3] = ty[2];
+        plan.header[4 + 3 * B] = 0u;  // split-item counter
       }
     }
   }
@@ -225,7 +226,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   const bool emit = final_mode && s >= out.first && oi < out.count;
   int32_t* orow = (emit && out.counts) ? out.counts + (size_t)oi * NB : nullptr;
   uint32_t* srow = st.counts + (size_t)s * ROW;
-  uint32_t g[9];
+  uint32_t g[9], nw = 0;
   if (!dirty) {
     // coalesced pass: lane l handles groups q = l + 64k (bins 4q..4q+3; 1798/1799 are
     // padding); even output rows are 16-B aligned and take one 16-B store per group
@@ -245,9 +246,16 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
         if (keep) store4_state(srow, b0, v);
       }
     }
-    // blocked group sums for the summary scan
+    // blocked group sums for the summary scan (and the merge-encoding words)
 #pragma unroll
-    for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
+    for (int q = 0; q < 9; ++q) {
+      g[q] = 0u;
+      if (q < ng) {
+        const uint4 v = lds.get4(28 * lane + 4 * q);
+        g[q] = sum4(v);
+        nw += merge_words4(v);
+      }
+    }
   } else {
     const SrcRow32 old{srow};
 #pragma unroll
@@ -259,6 +267,7 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
         const uint4 o = old.get4(b0);
         const uint4 cmb = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
         g[q] = sum4(cmb);
+        nw += merge_words4(cmb);
         if (orow) store4_1798(orow, b0, cmb);
         store4_state(srow, b0, cmb);  // the merged row is also the summary source
       }
@@ -271,14 +280,11 @@ __device__ __forceinline__ void emit_series(const SrcL& lds, uint32_t s, uint64_
   if (lane == 0 && emit && out.totals) out.totals[oi] = total;
   if (emit) {
     Summary88* so = out.summ ? out.summ + oi : nullptr;
-    uint32_t* wo = out.words ? out.words + oi : nullptr;
-    if (dirty) {
+    put_words(nw, out.words ? out.words + oi : nullptr);
+    if (dirty)
       wave_summary(g, SrcRow32{srow}, total, tb.mid, so);
-      row_words(SrcRow32{srow}, wo);
-    } else {
+    else
       wave_summary(g, lds, total, tb.mid, so);
-      row_words(lds, wo);
-    }
   }
 }
 
@@ -422,10 +428,23 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   };
   const uint4* __restrict__ citem = plan.cold_item;
   const uint32_t last = cold_items - 1u;
-  if (blockIdx.x < cold_items) fetch(citem[blockIdx.x]);
-  uint4 cn = citem[min(blockIdx.x + gridDim.x, last)];  // the next item's entry, in flight
+  // Items: a workgroup's first two are blockIdx.x and blockIdx.x + G; the rest come from
+  // a counter (2G, 2G + 1, ... in the order workgroups ask), so a workgroup that starts
+  // late -- its CU held by a k_accum_split workgroup -- takes fewer.  Each index is asked
+  // for two items ahead (the entry is loaded one item ahead) and passed through LDS.
+  __shared__ uint32_t s_next[2];
+  uint32_t* const ctr = plan.header + 2;  // zeroed by k_plan_b
+  const uint32_t G2 = 2u * gridDim.x;
+#if defined(L5DH_EXP) && (L5DH_EXP & 64)
+  if (threadIdx.x == 0) s_next[0] = blockIdx.x + G2;
+#else
+  if (threadIdx.x == 0) s_next[0] = G2 + atomicAdd(ctr, 1u);
+#endif
+  uint32_t item = blockIdx.x, item1 = blockIdx.x + gridDim.x;
+  if (item < cold_items) fetch(citem[item]);
+  uint4 cn = citem[min(item1, last)];  // the next item's entry, in flight
   __syncthreads();
-  for (uint32_t item = blockIdx.x; item < cold_items; item += gridDim.x) {
+  for (int par = 0; item < cold_items; par ^= 1) {
     const uint32_t tc = t;
     const bool dc = dirty;
     if (threadIdx.x < TILE) {
@@ -472,7 +491,14 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     }
     __syncthreads();  // counts complete; fixl visible
     fetch(cn);  // (past the last item: a harmless refetch of the last entry)
-    cn = citem[min(item + 2u * gridDim.x, last)];
+    const uint32_t item2 = s_next[par];
+    cn = citem[min(item2, last)];
+    uint32_t asked = 0;
+#if defined(L5DH_EXP) && (L5DH_EXP & 64)
+    if (threadIdx.x == 0) asked = item2 + gridDim.x;
+#else
+    if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);  // (stored at the end of the emission)
+#endif
     const uint32_t s0 = tc * TILE;
     // linear emission: a clean whole tile inside the output range of a resetting
     // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
@@ -511,11 +537,18 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
         const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
         if (linear) {
           const int ng = lane_groups(lane);
-          uint32_t g[9];
+          uint32_t g[9], nw = 0;
 #pragma unroll
-          for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(SrcLds16{row}.get4(28 * lane + 4 * q)) : 0u;
+          for (int q = 0; q < 9; ++q) {
+            g[q] = 0u;
+            if (q < ng) {
+              const uint4 v = SrcLds16{row}.get4(28 * lane + 4 * q);
+              g[q] = sum4(v);
+              nw += merge_words4(v);
+            }
+          }
+          put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
           wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
-          row_words(SrcLds16{row}, out.words ? out.words + (s - out.first) : nullptr);
           if (lane == 0 && out.totals) out.totals[s - out.first] = (int64_t)vsum + fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
@@ -536,8 +569,13 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
         linear_stores(true);
       }
     }
-    if (threadIdx.x == 0) st.dirty[tc] = keep ? 1 : 0;
-    __syncthreads();  // rows cleared, fixl consumed
+    if (threadIdx.x == 0) {
+      st.dirty[tc] = keep ? 1 : 0;
+      s_next[par ^ 1] = asked;
+    }
+    __syncthreads();  // rows cleared, fixl consumed, the next index visible
+    item = item1;
+    item1 = item2;
   }
 }
 
@@ -685,7 +723,10 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
   auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); };
   auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); };
-  for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+  // items: blockIdx.x first, then from a counter (G, G + 1, ...) as workgroups finish
+  __shared__ uint32_t s_item;
+  uint32_t* const ctr = plan.header + 4 + 3 * ((F + 1023) / 1024);  // zeroed by k_plan_b
+  for (uint32_t item = blockIdx.x; item < nitems; item = s_item) {
     const uint2 it = plan.split_item[item];
     const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
     {
@@ -760,9 +801,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
         const SrcLds32 src{hist + w * HROW};
         const int64_t total = (int64_t)my_vsum + st.sumfix[s];
         uint32_t g[9];
-        row_pass(src, g, out.counts + (size_t)s * NB);
+        row_pass(src, g, out.counts + (size_t)s * NB, out.words ? out.words + s : nullptr);
         wave_summary(g, src, total, tb.mid, out.summ ? out.summ + s : nullptr);
-        row_words(src, out.words ? out.words + s : nullptr);
         if (lane == 0) {
           st.sumfix[s] = 0;
           st.total[s] = total;
@@ -783,7 +823,12 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       }
       if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
     }
-    __syncthreads();  // the LDS rows are read: the next item may clear them
+#if defined(L5DH_EXP) && (L5DH_EXP & 64)
+    if (threadIdx.x == 0) s_item = item + gridDim.x;
+#else
+    if (threadIdx.x == 0) s_item = gridDim.x + atomicAdd(ctr, 1u);
+#endif
+    __syncthreads();  // the LDS rows are read: the next item may clear them; the next index visible
   }
 }
 
@@ -808,14 +853,12 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
           uint32_t* wo = out.words ? out.words + oi : nullptr;
           if (direct_out && !(plan.tile_flags[t] & TF_DIRTY)) {  // counted in the output row itself
             const SrcExt src{out.counts + (size_t)oi * NB};
-            row_pass(src, g, nullptr);
+            row_pass(src, g, nullptr, wo);
             wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
-            row_words(src, wo);
           } else {
             const SrcRow32 src{st.counts + (size_t)s * ROW};
-            row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr);
+            row_pass(src, g, out.counts ? out.counts + (size_t)oi * NB : nullptr, wo);
             wave_summary(g, src, total, tb.mid, out.summ ? out.summ + oi : nullptr);
-            row_words(src, wo);
           }
           if (lane == 0 && out.totals) out.totals[oi] = total;
         }
@@ -852,9 +895,8 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
   if (dirty) {
     const SrcRow32 src{st.counts + (size_t)s * ROW};
     const int64_t total = st.total[s];
-    row_pass(src, g, orow);
+    row_pass(src, g, orow, out.words ? out.words + i : nullptr);
     if (out.summ) wave_summary(g, src, total, tb.mid, out.summ + i);
-    row_words(src, out.words ? out.words + i : nullptr);
     if (totals_out && lane == 0) totals_out[i] = total;
     if (reset) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
