@@ -44,7 +44,7 @@ def main():
     settings = [("default", {}), ("hot_chunk=16384", {N.PARAM_HOT_CHUNK: 16384}),
                 ("direct_max=0", {N.PARAM_DIRECT_MAX: 0}), ("region_pct=40", {N.PARAM_REGION_PCT: 40}),
                 ("variant=4", {N.PARAM_VARIANT: 4}), ("variant=8", {N.PARAM_VARIANT: 8}),
-                ("variant=12", {N.PARAM_VARIANT: 12}), ("variant=8,region_pct=40", {N.PARAM_VARIANT: 8, N.PARAM_REGION_PCT: 40})]
+                ("variant=12", {N.PARAM_VARIANT: 12}), ("variant=12,region_pct=40", {N.PARAM_VARIANT: 12, N.PARAM_REGION_PCT: 40}), ("variant=8,region_pct=40", {N.PARAM_VARIANT: 8, N.PARAM_REGION_PCT: 40})]
     if len(sys.argv) > 2:
         settings = [x for x in settings if x[0] in sys.argv[2].split(";")]
     for name, prm in settings:
