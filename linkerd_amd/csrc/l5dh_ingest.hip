@@ -31,7 +31,7 @@ namespace l5dh {
 namespace {
 
 constexpr uint32_t RSAMPLE = 1u << 20;  // sampled ids per batch
-constexpr int RS_WG = 64;               // k_rsample workgroups (<= 16384 draws each: u16 LDS counters)
+constexpr int RS_WG = 256;              // k_rsample workgroups (<= 4096 draws each: u16 LDS counters)
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
