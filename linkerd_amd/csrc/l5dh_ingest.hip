@@ -33,6 +33,7 @@ namespace {
 constexpr uint32_t RSAMPLE = 1u << 20;  // sampled ids per batch
 constexpr int RS_WG = 256;              // k_rsample workgroups (<= 4096 draws each: u16 LDS counters)
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
+constexpr size_t RPLAN1_LDS = 32 * 1024 * 4;  // k_rplan1's per-tile sampled ids
 
 __device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   __shared__ uint32_t capl[BIN1_BINS];
   __shared__ double predl[BIN1_BINS];
   __shared__ unsigned long long best[16];
+  extern __shared__ uint32_t tel[];  // [32][1024]: sampled ids of tile t0 + k at tel[k * 1024 + j]
   const MetaLayout L = meta_layout(F);
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t NW = (F + 31) / 32;
@@ -135,11 +137,33 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   if (j < 33) lh[j] = 0;
   capl[j] = 0;
   predl[j] = 0.0;
-  __syncthreads();
-  auto tile_est = [&](int k) -> uint32_t {  // sampled ids of this thread's tile t0 + k
-    const uint32_t t = t0 + k;
-    return t < F ? kest[2 * t] + kest[2 * t + 1] : 0u;
+  // this thread's 32 tiles (64 consecutive key words) read once, all 16-B loads in
+  // flight together (a ragged end word by word), kept in LDS for the passes below
+  auto tile_pairs = [&](const uint32_t* __restrict__ kw, auto&& put) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // two batches of 8 loads (bounded registers)
+      uint4 x[8];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t t = t0 + 2 * (8 * h + g);
+        x[g] = make_uint4(0u, 0u, 0u, 0u);
+        if (t + 1 < F) {
+          x[g] = *reinterpret_cast<const uint4*>(kw + 2 * t);
+        } else if (t < F) {
+          x[g].x = kw[2 * t];
+          x[g].y = kw[2 * t + 1];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        put(2 * (8 * h + g), x[g].x + x[g].y);
+        put(2 * (8 * h + g) + 1, x[g].z + x[g].w);
+      }
+    }
   };
+  tile_pairs(kest, [&](int k, uint32_t v) { tel[k * 1024 + j] = v; });
+  __syncthreads();
+  auto tile_est = [&](int k) -> uint32_t { return tel[k * 1024 + j]; };  // sampled ids of tile t0 + k
   uint32_t dbits = 0;
   for (int k = 0; k < 32; ++k) {
     const double est = (double)tile_est(k) * s;
@@ -186,13 +210,12 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   // super-tile bins: this thread's non-direct tiles, summed with its partner (the other
   // half of the super-tile is lane j ^ 1 of the same wave)
   double P = 0.0, E = 0.0;
-  for (int k = 0; k < 32; ++k) {
-    const uint32_t t = t0 + k;
-    if (t < F && !((dbits >> k) & 1u)) {
-      P += (double)kprev[2 * t] + (double)kprev[2 * t + 1];
+  tile_pairs(kprev, [&](int k, uint32_t v) {
+    if (t0 + k < F && !((dbits >> k) & 1u)) {
+      P += (double)v;
       E += (double)tile_est(k);
     }
-  }
+  });
   P += __shfl_xor(P, 1, 64);
   E += __shfl_xor(E, 1, 64);
   if ((j & 1u) == 0 && (j >> 1) < FS) {
@@ -1114,6 +1137,8 @@ hipError_t set_ingest_attributes() {
   hipError_t e;
   if ((e = hipFuncSetAttribute((const void*)k_rsample, hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4)))
     return e;
+  if ((e = hipFuncSetAttribute((const void*)k_rplan1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RPLAN1_LDS)))
+    return e;
   if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)rbin1_lds(CH1))))
     return e;
@@ -1133,8 +1158,8 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
     case 0:  // sample + level-1 plan
       hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
                          a.kest);
-      hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32, a.thr_min,
-                         a.dmax, a.pct);
+      hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
+                         a.thr_min, a.dmax, a.pct);
       break;
     case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
       for (int pass = 0; pass < 2; ++pass) {
