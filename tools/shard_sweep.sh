@@ -1,6 +1,6 @@
 #!/bin/bash
 # One C3 shard sweep: each rank's shard of a W-way split (bench.py --shard r/W) on
-# this one GPU, for the COST_CALIBRATION of bench.py.  tools/shard_sweep.sh <tag> [W]
+# this one GPU (the load-derived plan of fleet.plan_shards).  tools/shard_sweep.sh <tag> [W]
 set -o pipefail
 TAG=$1; W=${2:-8}
 mkdir -p gpurun_out/sw_$TAG
