@@ -180,6 +180,14 @@ int l5dh_summarize_dense(l5dh_ctx* ctx, const int32_t* counts, const int64_t* to
 int l5dh_comm_unique_id(void* id_out /* L5DH_UNIQUE_ID_BYTES */);
 int l5dh_comm_init_rank(l5dh_ctx* ctx, const void* id, int nranks, int rank);
 int l5dh_comm_init_all(l5dh_ctx** ctxs, int n);
+/* Test transport: n contexts on ONE device form an n-rank group whose collectives are
+ * device copies and reductions among their buffers (no RCCL), so the multi-rank merge
+ * code -- per-destination slices, the size all-gather, the payload exchange, the
+ * in-place local slice, the decode -- runs on a single GPU.  Such a group merges
+ * through l5dh_merge_all only.  At most 64 ranks for every communicator kind
+ * (the sparse reduce-scatter's sources): larger groups are rejected here, before
+ * any merge consumes an interval. */
+int l5dh_comm_init_loopback(l5dh_ctx** ctxs, int n);
 int l5dh_comm_destroy(l5dh_ctx* ctx);
 
 /* Reference: the snapshot of a series whose samples arrived on several hosts

@@ -59,8 +59,11 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     private[this] val ticket = Array(0L, 0L) // l5dh_ingest_async ticket of each pair (0: free)
     private[this] var cur = 0
     private[this] var n = 0
+    private[this] var closed = false // the pinned buffers went back to the library (free)
 
     def add(id: Int, value: Float): Unit = synchronized {
+      // a thread adding after (or racing with) close() must not write freed native memory
+      if (closed) throw new IllegalStateException("GpuEngine is closed")
       ids(cur).putInt(4 * n, id)
       values(cur).putFloat(4 * n, value)
       n += 1
@@ -68,7 +71,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     }
 
     /** Everything staged reaches the library; returns once both buffers are free. */
-    def flush(): Unit = synchronized(flushLocked(waitAll = true))
+    def flush(): Unit = synchronized { if (!closed) flushLocked(waitAll = true) }
 
     private[this] def flushLocked(waitAll: Boolean): Unit = {
       if (n > 0) {
@@ -89,8 +92,11 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
 
     /** After a final flush: the pinned buffers go back to the library. */
     def free(): Unit = synchronized {
-      flushLocked(waitAll = true)
-      for (b <- ids ++ values) Native.pinFree(b)
+      if (!closed) {
+        closed = true // first: a failing flush still leaves the Staging closed
+        try flushLocked(waitAll = true)
+        finally for (b <- ids ++ values) Native.pinFree(b)
+      }
     }
   }
 
@@ -176,11 +182,12 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
   }
 
   def close(): Unit = {
-    val it = stagings.iterator
-    while (it.hasNext) it.next.free() // every thread's staging: flushed, then its pinned buffers freed
-    stagings.clear()
-    check(Native.sync(ctx), "l5dh_sync")
-    check(Native.close(ctx), "l5dh_close")
+    try {
+      val it = stagings.iterator
+      while (it.hasNext) it.next.free() // every thread's staging: flushed, closed, its pinned buffers freed
+      stagings.clear()
+      check(Native.sync(ctx), "l5dh_sync") // may report a deferred invalid-id -EINVAL (ABI 3)
+    } finally check(Native.close(ctx), "l5dh_close") // the context is released even then
   }
 }
 

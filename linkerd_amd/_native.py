@@ -88,6 +88,7 @@ SIGNATURES = {
     "l5dh_comm_unique_id": (_c.c_int, [_vp]),
     "l5dh_comm_init_rank": (_c.c_int, [_vp, _vp, _c.c_int, _c.c_int]),
     "l5dh_comm_init_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int]),
+    "l5dh_comm_init_loopback": (_c.c_int, [_c.POINTER(_vp), _c.c_int]),
     "l5dh_comm_destroy": (_c.c_int, [_vp]),
     "l5dh_merge": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
     "l5dh_tile_totals": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.c_size_t]),

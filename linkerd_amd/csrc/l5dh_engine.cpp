@@ -222,6 +222,7 @@ struct l5dh_ctx {
   std::vector<uint64_t> m_to, m_from;  // words to / from every rank
   uint64_t m_dense_bytes = 0, m_encoded_bytes = 0, m_sent_bytes = 0;
   bool rccl_1rank = false;  // run the collective in a 1-rank communicator too (an identity otherwise skipped)
+  bool loopback = false;    // l5dh_comm_init_loopback: the collectives are device copies among the group's contexts
   uint32_t variant = 0;  // L5DH_PARAM_VARIANT: result-preserving kernel variants (A/B timing)
   // params
   uint32_t cold_limit = COLD_LIMIT_MAX;
@@ -360,7 +361,6 @@ Segs segs_view(l5dh_ctx* c) {
   Segs s{};
   s.n = c->nseg;
   for (int j = 0; j < c->nseg; ++j) {
-    s.rec32[j] = static_cast<const uint32_t*>(c->segs[j].rec32.p);
     s.rec16[j] = static_cast<const uint16_t*>(c->segs[j].rec16.p);
     s.meta[j] = c->segs[j].meta;
   }
@@ -409,12 +409,12 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
     if (split_items) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) != 0, c->side));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, (c->variant & 16) != 0, c->stream));
+      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));
     }
   }
   if (hot) {
@@ -476,8 +476,12 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   // region buffers: the plan sizes the regions from the previous batch and a sample
   // of this one, with slack; a plan that does not fit is scaled to these sizes (an
   // overflowing region is then redone with exact sizes, which always fit)
+  // rec32: the super-tile bins' records; rec16: the direct keys' regions in [0, dlim16)
+  // (planned, so possibly oversized) and level 2's regions after them, with room for
+  // level 2's exact layout in any case (N + 7 per key of padding)
   const size_t cap32 = n + n / 2 + ((size_t)1 << 19);
-  const size_t cap16 = n + n / 2 + (size_t)64 * 2 * c->F;
+  const size_t cap16 = 2 * n + n / 8 + (size_t)128 * c->F + 4096;
+  const size_t dlim16 = cap16 - (n + (size_t)16 * c->F + 1024);
   {
     int r = ensure(c, sg.rec32, (cap32 + 16) * 4);  // readers load whole 16-B groups
     if (!r) r = ensure(c, sg.rec16, (cap16 + 16) * 2);
@@ -509,12 +513,12 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   a.rec16 = static_cast<uint16_t*>(sg.rec16.p);
   a.cap32 = cap32;
   a.cap16 = cap16;
+  a.dlim16 = dlim16;
   a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
   const uint32_t FS = (c->F + 63) / 64;
   a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + the trash bin
   a.pct = c->region_pct;
   a.vec = vec;
-  a.l1 = (int)((c->variant >> 2) & 3u);  // variant bits 3:2: the level-1 kernel (A/B timing)
   {
     KTimer kt(c, L5DH_K_SCAN);
     HIPCHK(c, launch_ingest(a, 0, c->stream));
@@ -681,7 +685,8 @@ uint32_t merge_per(const l5dh_ctx* c) { return (c->S + c->nranks - 1) / c->nrank
 // Phase 1: pending samples + state -> dense rows [Sp][1798] and totals [Sp] (the
 // fused whole-range export with reset), pad rows zero.
 int merge_export(l5dh_ctx* c) {
-  if (!c->comm) return fail(c, -EINVAL, "no communicator: call l5dh_comm_init_rank or l5dh_comm_init_all first");
+  if (!c->comm && !c->loopback)
+    return fail(c, -EINVAL, "no communicator: call l5dh_comm_init_rank or l5dh_comm_init_all first");
   int r = flush_ring(c);
   if (r) return r;
   const size_t Sp = (size_t)merge_per(c) * c->nranks;
@@ -889,9 +894,84 @@ int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, 
   return sync_stream(c);
 }
 
+// The loopback group's collectives (l5dh_comm_init_loopback: n contexts on one device):
+// the same encode / size / receive / payload steps as over RCCL, with each exchange
+// done by device copies (all streams drained first) and the reductions by one kernel
+// reading every rank's buffer.
+int sync_all(l5dh_ctx** cs, int n) {
+  for (int i = 0; i < n; ++i) HIPCHK(cs[i], hipStreamSynchronize(cs[i]->stream));
+  return 0;
+}
+
+int loop_collectives(l5dh_ctx** cs, int n, int mode) {
+  int r;
+  const int W = n;
+  const uint32_t per = merge_per(cs[0]);
+  if (mode != L5DH_MERGE_REDUCE_SCATTER) {  // dense all-reduce: the sum into rank 0's rows, copied to the others
+    const size_t Sp = (size_t)per * W;
+    if ((r = sync_all(cs, n))) return r;
+    std::vector<const int32_t*> rows(W);
+    std::vector<const int64_t*> tots(W);
+    for (int i = 0; i < W; ++i) {
+      rows[i] = static_cast<const int32_t*>(cs[i]->merge_counts.p);
+      tots[i] = static_cast<const int64_t*>(cs[i]->merge_totals.p);
+    }
+    l5dh_ctx* c0 = cs[0];
+    HIPCHK(c0, merge_loop_sum_i32(rows.data(), W, static_cast<int32_t*>(c0->merge_counts.p), Sp * NB, c0->stream));
+    HIPCHK(c0, merge_loop_sum_i64(tots.data(), W, static_cast<int64_t*>(c0->merge_totals.p), Sp, c0->stream));
+    HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    for (int i = 1; i < W; ++i) {
+      HIPCHK(cs[i], hipMemcpyAsync(cs[i]->merge_counts.p, c0->merge_counts.p, Sp * NB * 4, hipMemcpyDeviceToDevice,
+                                   cs[i]->stream));
+      HIPCHK(cs[i], hipMemcpyAsync(cs[i]->merge_totals.p, c0->merge_totals.p, Sp * 8, hipMemcpyDeviceToDevice,
+                                   cs[i]->stream));
+    }
+    for (int i = 0; i < W; ++i) {
+      cs[i]->m_dense_bytes = cs[i]->m_encoded_bytes = Sp * (NB * 4 + 8);
+      cs[i]->m_sent_bytes = 2 * cs[i]->m_dense_bytes * (W - 1) / W;
+    }
+    return sync_all(cs, n);
+  }
+  for (int i = 0; i < n; ++i)
+    if ((r = merge_encode_step(cs[i]))) return r;
+  if ((r = sync_all(cs, n))) return r;
+  for (int i = 0; i < n; ++i)  // all-gather of the size rows
+    for (int j = 0; j < n; ++j)
+      if (j != i)
+        HIPCHK(cs[j], hipMemcpyAsync(static_cast<uint64_t*>(cs[j]->m_sizes.p) + (size_t)i * W,
+                                     static_cast<const uint64_t*>(cs[i]->m_sizes.p) + (size_t)i * W, (size_t)W * 8,
+                                     hipMemcpyDeviceToDevice, cs[j]->stream));
+  for (int i = 0; i < n; ++i)
+    if ((r = merge_recv_step(cs[i]))) return r;
+  if ((r = sync_all(cs, n))) return r;
+  for (int q = 0; q < W; ++q) {  // destination q receives every other source's slice q
+    l5dh_ctx* d = cs[q];
+    uint64_t rat = 0;
+    for (int p = 0; p < W; ++p) {
+      l5dh_ctx* sp = cs[p];
+      if (p != q) {
+        uint64_t at = 0;
+        for (int k = 0; k < q; ++k) at += sp->m_to[k];
+        if (sp->m_to[q])
+          HIPCHK(d, hipMemcpyAsync(static_cast<uint32_t*>(d->r_enc.p) + rat, static_cast<const uint32_t*>(sp->m_enc.p) + at,
+                                   sp->m_to[q] * 4, hipMemcpyDeviceToDevice, d->stream));
+        HIPCHK(d, hipMemcpyAsync(static_cast<uint32_t*>(d->r_words.p) + (size_t)p * per,
+                                 static_cast<const uint32_t*>(sp->m_words.p) + (size_t)q * per, (size_t)per * 4,
+                                 hipMemcpyDeviceToDevice, d->stream));
+      }
+      rat += d->m_from[p];
+    }
+    std::vector<const int64_t*> tots(W);  // the totals' reduce-scatter: slice q summed over the sources
+    for (int p = 0; p < W; ++p) tots[p] = static_cast<const int64_t*>(cs[p]->merge_totals.p) + (size_t)q * per;
+    HIPCHK(d, merge_loop_sum_i64(tots.data(), W, static_cast<int64_t*>(d->recv_totals.p), per, d->stream));
+  }
+  return sync_all(cs, n);
+}
+
 // The collective steps of one merge over contexts `cs` (one, or every context of an
 // l5dh_comm_init_all communicator): each collective step is grouped over them.
 int merge_collectives(l5dh_ctx** cs, int n, int mode) {
+  if (cs[0]->loopback) return loop_collectives(cs, n, mode);
   int r = 0;
   if (mode != L5DH_MERGE_REDUCE_SCATTER) {
     NCCLCHK(cs[0], ncclGroupStart());
@@ -1360,7 +1440,9 @@ int l5dh_comm_unique_id(void* id_out) {
 int l5dh_comm_init_rank(l5dh_ctx* c, const void* id, int nranks, int rank) {
   if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->comm) return fail(c, -EINVAL, "context already has a communicator");
+  if (c->comm || c->loopback) return fail(c, -EINVAL, "context already has a communicator");
+  // (the sparse reduce-scatter holds one source per rank: checked before any merge runs)
+  if (nranks > MERGE_MAX_RANKS) return fail(c, -EINVAL, "fleet merge: more than 64 ranks");
   hipSetDevice(c->device);
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
@@ -1373,10 +1455,10 @@ int l5dh_comm_init_rank(l5dh_ctx* c, const void* id, int nranks, int rank) {
 }
 
 int l5dh_comm_init_all(l5dh_ctx** ctxs, int n) {
-  if (!ctxs || n < 1) return -EINVAL;
+  if (!ctxs || n < 1 || n > MERGE_MAX_RANKS) return -EINVAL;
   std::vector<int> devs(n);
   for (int i = 0; i < n; ++i) {
-    if (!ctxs[i] || ctxs[i]->comm || ctxs[i]->S != ctxs[0]->S) return -EINVAL;
+    if (!ctxs[i] || ctxs[i]->comm || ctxs[i]->loopback || ctxs[i]->S != ctxs[0]->S) return -EINVAL;
     devs[i] = ctxs[i]->device;
   }
   std::vector<ncclComm_t> comms(n, nullptr);
@@ -1394,6 +1476,24 @@ int l5dh_comm_init_all(l5dh_ctx** ctxs, int n) {
   return 0;
 }
 
+int l5dh_comm_init_loopback(l5dh_ctx** ctxs, int n) {
+  if (!ctxs || n < 1 || n > MERGE_MAX_RANKS) return -EINVAL;
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i] || ctxs[i]->comm || ctxs[i]->loopback || ctxs[i]->S != ctxs[0]->S ||
+        ctxs[i]->device != ctxs[0]->device)
+      return -EINVAL;
+    for (int j = 0; j < i; ++j)
+      if (ctxs[j] == ctxs[i]) return -EINVAL;
+  }
+  for (int i = 0; i < n; ++i) {
+    std::lock_guard<std::mutex> g(ctxs[i]->mu);
+    ctxs[i]->loopback = true;
+    ctxs[i]->nranks = n;
+    ctxs[i]->rank = i;
+  }
+  return 0;
+}
+
 int l5dh_comm_destroy(l5dh_ctx* c) {
   if (!c) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -1403,6 +1503,7 @@ int l5dh_comm_destroy(l5dh_ctx* c) {
     if (r) return r;
     ncclCommDestroy(c->comm);
   }
+  c->loopback = false;
   c->comm = nullptr;
   c->nranks = 1;
   c->rank = 0;
@@ -1414,6 +1515,7 @@ int l5dh_merge(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, in
   if (!c || (mode != L5DH_MERGE_REDUCE_SCATTER && mode != L5DH_MERGE_ALL_REDUCE)) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
+  if (c->loopback) return fail(c, -EINVAL, "a loopback group merges through l5dh_merge_all");
   int r;
   if ((r = merge_export(c))) return r;
   if ((r = merge_collectives(&c, 1, mode))) return r;
@@ -1424,7 +1526,9 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
                    uint32_t* firsts, uint32_t* counts) {
   if (!ctxs || n < 1 || (mode != L5DH_MERGE_REDUCE_SCATTER && mode != L5DH_MERGE_ALL_REDUCE)) return -EINVAL;
   for (int i = 0; i < n; ++i)
-    if (!ctxs[i] || !ctxs[i]->comm || ctxs[i]->nranks != n || ctxs[i]->rank != i) return -EINVAL;
+    if (!ctxs[i] || !(ctxs[i]->comm || ctxs[i]->loopback) || ctxs[i]->loopback != ctxs[0]->loopback ||
+        ctxs[i]->nranks != n || ctxs[i]->rank != i)
+      return -EINVAL;
   std::vector<std::unique_lock<std::mutex>> locks;
   for (int i = 0; i < n; ++i) locks.emplace_back(ctxs[i]->mu);  // in rank order
   int r;

@@ -6,12 +6,13 @@
 //   k_rplan1   this batch's direct tiles (the biggest estimated) and the level-1 bin
 //              regions (super-tiles; two half-bins per direct tile), sized from the
 //              previous batch's exact key counts and this batch's sample
-//   k_rbin1    level 1: LDS counting sort of 16K-sample sub-chunks by bin; each run's
+//   k_rbin1w   level 1: LDS counting sort of 24K-sample sub-chunks by bin; each run's
 //              place in its bin's region comes from ONE returning global atomic per
 //              (sub-chunk, bin) on the bin's cursor (order inside a region is free:
-//              integer sums do not depend on it)
+//              integer sums do not depend on it); direct tiles' samples bucketized
+//              into their final u16 records, their value sums folded in LDS
 //   k_rfix1    a run that did not fit its region -> exact regions from the cursors
-//              and a second k_rbin1 pass (launched always, it exits unless needed);
+//              and a second k_rbin1w pass (launched always, it exits unless needed);
 //              the direct keys' ranges; the invalid-id count to the host
 //   k_rplan2a/b level-2 regions of the other keys; level-2 items (16K records of a
 //              super-tile's level-1 region)
@@ -20,9 +21,11 @@
 //   k_rfix2a/b exact key counts -> kprev (the next batch's prediction); overflow ->
 //              exact regions and a second k_rbin2 pass
 //
-// Level-1 record (rec32): [31:26] tile in super-tile | [25:21] series in tile |
-//   [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped: the exact sum
-//   contribution went to sumfix[series], integer atomics, order free).
+// Level-1 record of a super-tile bin (rec32): [31:26] tile in super-tile | [25:21]
+//   series in tile | [20:0] payload = v (0 <= v < V_ESC) or V_ESC + bucket (escaped:
+//   the exact sum contribution went to sumfix[series], integer atomics, order free).
+// Final record (rec16, direct tiles at level 1, the others at level 2): [15:11]
+//   series in tile | [10:0] bucket.
 #include <algorithm>
 
 #include "l5dh_device.hpp"
@@ -117,7 +120,8 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
 // least max(thr_min, 2^k), k the smallest power keeping <= dmax of them.
 __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
-                                                 size_t cap32, uint32_t thr_min, uint32_t dmax, uint32_t pct) {
+                                                 size_t cap32, size_t dlim16, uint32_t thr_min, uint32_t dmax,
+                                                 uint32_t pct) {
   __shared__ uint32_t lh[33];
   __shared__ uint32_t sthr;
   __shared__ uint4 lds4[17];
@@ -228,18 +232,24 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   if (j >= FS && j < TB) {  // direct half-bins
     const uint32_t t = dl[(j - FS) >> 1], h = (j - FS) & 1u;
     const double p = (double)kprev[2 * t + h], e = (double)kest[2 * t + h];
-    capl[j] = rcap(p, e, s, exact, 256.0, 4, pct);
+    capl[j] = rcap(p, e, s, exact, 256.0, 8, pct);  // (u16 records: 16-B aligned regions)
     predl[j] = fmax(p, e * s);
   }
   __syncthreads();
-  uint64_t total;
-  const uint64_t base = block_excl_scan64((uint64_t)capl[j], l64, &total);
-  if (base + capl[j] + 16 > cap32)  // past the buffer's end: clamped (its runs overflow; level 1 is redone exactly)
-    capl[j] = base + 16 < cap32 ? (uint32_t)(cap32 - 16 - base) & ~3u : 0u;
+  // two address spaces: super-tile bins in rec32, the direct half-bins in rec16 below
+  // dlim16 (the rest of rec16 stays free for level 2's exact worst case)
+  const bool stb = j < FS, dj = j >= FS && j < TB;
+  uint64_t tot32, tot16;
+  const uint64_t base32 = block_excl_scan64(stb ? (uint64_t)capl[j] : 0ull, l64, &tot32);
+  const uint64_t base16 = block_excl_scan64(dj ? (uint64_t)capl[j] : 0ull, l64, &tot16);
+  const uint64_t base = stb ? base32 : base16;
+  const uint64_t lim = stb ? cap32 : dlim16;
+  if (base + capl[j] + 16 > lim)  // past the space's end: clamped (its runs overflow; level 1 is redone exactly)
+    capl[j] = base + 16 < lim ? (uint32_t)(lim - 16 - base) & (stb ? ~3u : ~7u) : 0u;
   meta[L.bbase() + j] = (uint32_t)base;
   meta[L.bcap() + j] = j < TB ? capl[j] : 0u;
   meta[L.bcnt() + j] = 0u;
-  // the two biggest bins by prediction, for the ballot ranking of k_rbin1
+  // the two biggest bins by prediction, for the ballot ranking of k_rbin1w
   const int lane = j & 63, w = j >> 6;
   auto block_max = [&](unsigned long long v) -> unsigned long long {
 #pragma unroll
@@ -275,235 +285,51 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
     hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
+    hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);
   }
 }
 
 // ------------------------------------------------------------------------
-// Level 1.  Bins: the FS super-tiles (their non-direct records, for level 2), two
-// half-bins per direct tile (final records), and a trash bin (slots with no valid
-// sample: the batch's ragged end, ids >= S) that is never written.  Per CH1-slot
-// sub-chunk: one LDS atomic ranks each slot in its bin (or a wave ballot, for the
-// two hottest bins when one holds >= half the batch), every wave reserves the runs
-// of 64 bins with one returning global atomic per non-empty bin, a one-wave scan
-// gives stage offsets, each slot is staged sorted with its bin, and the stage is
-// written in order to run base + position.  pass 1 (the redo) exits unless k_rfix1
-// asked for it and adds nothing to sumfix or the error counter.
-// LDS: stage[CH1] uint2, cnt[BINS], ocx[BINS] {stage offset, run base}, direct words.
-constexpr size_t rbin1_lds(int ch) { return (size_t)ch * 8 + BIN1_BINS * 12 + 1024 * 8 + 16; }
-
-template <int CH1, int NT>
-__global__ __launch_bounds__(NT, 1) void k_rbin1(const uint32_t* __restrict__ series, const float* __restrict__ values,
-                                                 size_t n, size_t per, uint32_t S, uint32_t F, Tables tb,
-                                                 uint32_t* __restrict__ meta, uint32_t* __restrict__ rec32,
-                                                 int64_t* __restrict__ sumfix, uint32_t* __restrict__ err, int vec,
-                                                 int pass) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint2* stage = reinterpret_cast<uint2*>(smem);          // [CH1] {record, bin}
-  uint32_t* cnt = smem + 2 * CH1;                         // [BIN1_BINS]
-  uint2* ocx = reinterpret_cast<uint2*>(cnt + BIN1_BINS); // [BIN1_BINS] {stage offset, run base | INVALID}
-  uint2* dw = ocx + BIN1_BINS;                            // [1024] {direct bits, direct tiles before}
-  const MetaLayout L = meta_layout(F);
-  uint32_t* hdr = meta + L.hdr();
-  if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
-  uint32_t* bcnt = meta + L.bcnt();
-  const uint32_t* bbase = meta + L.bbase();
-  const uint32_t* bcap = meta + L.bcap();
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t NW = (F + 31) / 32;
-  const uint32_t ND = hdr[H_ND];
-  const uint32_t TB = FS + 2 * ND;
-  const bool hotrank = hdr[H_HS] != 0u;
-  const uint32_t hb0 = hdr[H_HB0], hb1 = hdr[H_HB1];
-  const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(meta[L.dbits() + w], meta[L.dpre() + w]);
-  for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) cnt[b] = 0;
-  __syncthreads();
-  const size_t lo = (size_t)blockIdx.x * per;
-  const size_t hi = lo + per < n ? lo + per : n;
-  bool bad = false;
-  constexpr int PT = CH1 / NT;  // slots per thread: PT/4 groups of 4 consecutive
-  for (size_t c0 = lo; c0 < hi; c0 += CH1) {
-    uint32_t sv[PT];
-    float fv[PT];
-    if (vec && c0 + CH1 <= hi) {
-#pragma unroll
-      for (int k = 0; k < PT / 4; ++k) {
-        const size_t base = c0 + 4 * ((size_t)k * NT + threadIdx.x);
-        const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
-        const float4 f4 = *reinterpret_cast<const float4*>(values + base);
-        sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
-        fv[4 * k] = f4.x; fv[4 * k + 1] = f4.y; fv[4 * k + 2] = f4.z; fv[4 * k + 3] = f4.w;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const size_t i = c0 + 4 * ((size_t)(k >> 2) * NT + threadIdx.x) + (k & 3);
-        const bool in = i < hi;
-        sv[k] = in ? series[i] : 0xFFFFFFFFu;
-        fv[k] = in ? values[i] : 0.0f;
-        bad |= in && sv[k] >= S;
-      }
-    }
-    // Per group of 4 slots: payloads (samples outside [0, V_ESC) take a rare path
-    // through this thread's still free stage slots), direct words, branch-free bins,
-    // one rank atomic per slot.
-    uint32_t rec[PT];
-    uint32_t pk[PT];  // [13:0] rank | [24:14] bin
-#pragma unroll
-    for (int g = 0; g < PT; g += 4) {
-      uint32_t pl[4];
-      uint32_t escm = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // fast: +0 <= f < V_ESC, one integer compare of the bit pattern (-0, NaN and
-        // (-1, 0) take the exact slow path, which also truncates them to 0)
-        const float f = fv[g + q];
-        const bool fast = __float_as_uint(f) < 0x49FFC000u;  // bits of (float)V_ESC
-        pl[q] = fast ? (uint32_t)f : 0u;
-        escm |= (!fast && sv[g + q] < S) ? (1u << q) : 0u;
-        if (vec && c0 + CH1 <= hi) bad |= sv[g + q] >= S;
-      }
-      if (__ballot(escm != 0u)) {
-        uint32_t* tmp = reinterpret_cast<uint32_t*>(stage) + threadIdx.x * 8;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          tmp[2 * q] = sv[g + q];
-          tmp[2 * q + 1] = __float_as_uint(fv[g + q]);
-        }
-#pragma unroll 1
-        for (int q = 0; q < 4; ++q)
-          if ((escm >> q) & 1u)
-            tmp[2 * q] = pass == 0 ? payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix)
-                                   : payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, nullptr);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if ((escm >> q) & 1u) pl[q] = tmp[2 * q];
-      }
-      uint2 dv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
-      uint32_t bn[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t s = sv[g + q];
-        const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);  // tile within its direct word
-        const bool direct = __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
-        rec[g + q] = ((s & (ST_TILES * TILE - 1)) << 21) | pl[q];  // tile in ST | series in tile | payload
-        const uint32_t dbin =
-            FS + 2u * (dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw))) + ((s >> 4) & 1u);
-        bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
-      }
-      if (!hotrank) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pk[g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 14);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pk[g + q] = bn[q] << 14;  // ranked below, all PT slots at once
-      }
-      asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
-    }
-    if (hotrank) {
-      // the batch's two hottest bins by wave ballots: one LDS atomic per wave and bin,
-      // consecutive stage slots; the other bins by one LDS atomic per slot
-      uint32_t wc0 = 0, wc1 = 0;
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const uint32_t b = pk[k] >> 14;
-        const bool m0 = b == hb0, m1 = b == hb1;
-        wc0 += (uint32_t)__popcll(__ballot(m0));
-        wc1 += (uint32_t)__popcll(__ballot(m1));
-        if (!m0 && !m1) pk[k] |= atomicAdd(cnt + b, 1u);
-      }
-      uint32_t base = 0;
-      if (lane == 0 && wc0) base = atomicAdd(cnt + hb0, wc0);
-      if (lane == 1 && wc1) base = atomicAdd(cnt + hb1, wc1);
-      uint32_t r0 = __builtin_amdgcn_readlane(base, 0), r1 = __builtin_amdgcn_readlane(base, 1);
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const uint32_t b = pk[k] >> 14;
-        const bool m0 = b == hb0, m1 = b == hb1;
-        const unsigned long long x0 = __ballot(m0), x1 = __ballot(m1);
-        if (m0) pk[k] |= r0 + mask_below(x0);
-        if (m1) pk[k] |= r1 + mask_below(x1);
-        r0 += (uint32_t)__popcll(x0);
-        r1 += (uint32_t)__popcll(x1);
-      }
-    }
-    __syncthreads();
-    // run reservations: wave w, lane l -> bin 64 w + l (one returning atomic per
-    // non-empty bin; the results are used only after the scan and the scatter)
-    const uint32_t rb_bin = (uint32_t)wv * 64u + (uint32_t)lane;
-    const uint32_t rc = rb_bin < TB ? cnt[rb_bin] : 0u;
-    uint32_t rold = 0, rbase = 0, rcapv = 0;
-    if (rc) {
-      rold = atomicAdd(&bcnt[rb_bin], rc);
-      rbase = bbase[rb_bin];
-      rcapv = bcap[rb_bin];
-    }
-    if (wv == 0) {  // one wave: the stage offsets (DPP scan of 16 bins per lane)
-      uint32_t c[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cnt + 16 * lane + 4 * q);
-        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
-      }
-      uint32_t tl = 0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) tl += c[q];
-      uint32_t e = wave_incl_scan32(tl) - tl;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        ocx[16 * lane + q].x = e;
-        e += c[q];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t bin = (pk[k] >> 14) & 2047u;
-      stage[ocx[bin].x + (pk[k] & 16383u)] = make_uint2(rec[k], bin);
-    }
-    {
-      uint32_t rb = INVALID;
-      if (rc) {
-        if (rold + rc <= rcapv) rb = rbase + rold;
-        else hdr[H_OV1] = 1u;  // this run is dropped; k_rfix1 has the batch redone with exact regions
-      }
-      ocx[rb_bin].y = rb;
-      cnt[rb_bin] = 0;  // (every reader of the counts is past the barrier above)
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {  // all CH1 entries, in sorted order (each wave a contiguous PT x 64 range)
-      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
-      const uint2 e = stage[i];
-      const uint2 o = ocx[e.y & 2047u];
-      if (o.y != INVALID) rec32[o.y + (i - o.x)] = e.x;
-    }
-    __syncthreads();
-  }
-  if (pass == 0 && bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
-}
-
-// ------------------------------------------------------------------------
-// Level 1 with 24K-slot sub-chunks (1.5x k_rbin1's, so runs 1.5x as long): the stage
-// holds records only (4 B), and each entry's bin is recovered at write-out from a run
-// head bitmap -- bit off[b] set for every non-empty bin b -- as the number of heads at
-// or before the entry: a per-64-entry group prefix (gpre) plus a popcount of the
-// group's 64 bits, indexing the runs' destination deltas (rdelta[run] = run base -
-// stage offset, or INVALID).  Same bins, ranking, reservations and redo as k_rbin1.
+// Level 1, one 768-thread workgroup per CU walking its slab in 24K-slot sub-chunks.
+// Bins: the FS super-tiles (u32 records with the value, for level 2), two half-bins
+// per direct tile (final u16 records: the sample is bucketized here, and its value
+// added to an LDS sum of its series), and a trash bin (slots with no valid sample:
+// the batch's ragged end, ids >= S) that is never written.  Per sub-chunk: one LDS
+// atomic ranks each slot in its bin (or a wave ballot, for the two hottest bins when
+// one holds >= half the batch), one returning global atomic per non-empty bin
+// reserves the sub-chunk's run in the bin's region, a one-wave scan gives stage
+// offsets and run ranks, the records are staged sorted (4 B each), and the stage is
+// written out in order: each entry's run is the number of run heads at or before
+// it -- a per-64-entry group prefix (gpre) plus a popcount of the group's bits of
+// the run-head bitmap -- indexing the runs' destination deltas (rdelta[run] = run
+// base - stage offset, or INVALID).  Runs below the first direct bin's rank are u32
+// records (rec32), the others u16 (rec16).  A run that does not fit is dropped and
+// flagged; pass 1 (the redo) exits unless k_rfix1 asked for it and adds nothing to
+// sumfix or the error counter.
+//
+// Direct value sums: u32 per direct series in LDS; an add that wraps past 2^32 adds
+// 2^32 to sumfix[series] (the wrapping lane is told by the atomic's return value),
+// and each workgroup adds its remainders to sumfix at the end of its slab.
+//
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
-// rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2.
+// rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
+// lut2 [1024] uint2, direct sums [255 x 32].
 constexpr int CHW = 24576;
-constexpr size_t rbin1w_lds(int ch) { return (size_t)ch * 4 + BIN1_BINS * 12 + ch / 8 + ch / 32 + 1024 * 8 + 16; }
+#ifndef L5DH_RBIN1_NT
+#define L5DH_RBIN1_NT 768
+#endif
+constexpr int NT1 = L5DH_RBIN1_NT;  // (development builds may set 1024: 24 slots per thread)
+constexpr int DSUM_N = DIRECT_MAX * TILE;
+constexpr size_t rbin1w_lds() {
+  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
+}
 
 template <int NT, int CH>
 __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ series, const float* __restrict__ values,
                                                   size_t n, size_t per, uint32_t S, uint32_t F, Tables tb,
                                                   uint32_t* __restrict__ meta, uint32_t* __restrict__ rec32,
-                                                  int64_t* __restrict__ sumfix, uint32_t* __restrict__ err, int vec,
-                                                  int pass) {
+                                                  uint16_t* __restrict__ rec16, int64_t* __restrict__ sumfix,
+                                                  uint32_t* __restrict__ err, int vec, int pass) {
   constexpr int PT = CH / NT;  // slots per thread, loaded and ranked in halves
   constexpr int PH = PT / 2;
   static_assert(PH % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
@@ -515,6 +341,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint32_t* heads = rdelta + BIN1_BINS;                          // [CH / 32] run heads
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
+  uint2* lut2 = dw + 1024;                                       // [LUT2_N]
+  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
   __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
@@ -533,6 +361,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const unsigned long long mle = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
   for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(meta[L.dbits() + w], meta[L.dpre() + w]);
   for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) cnt[b] = 0;
+  for (uint32_t i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+  for (uint32_t i = threadIdx.x; i < ND * TILE; i += NT) dsum[i] = 0;
   __syncthreads();
   // (a batch piece holds < 2^30 samples: 32-bit sample indices)
   const uint32_t lo = (uint32_t)((size_t)blockIdx.x * per);
@@ -540,7 +370,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   bool bad = false;
   for (uint32_t c0 = lo; c0 < hi; c0 += CH) {
     for (uint32_t wd = threadIdx.x; wd < CH / 32; wd += NT) heads[wd] = 0u;
-    uint32_t rec[PT];
+    // records are staged in slot order first (the stage is free until the scatter), so
+    // only their ranks and bins stay in registers while the sub-chunk is ranked
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
 #pragma unroll
@@ -572,6 +403,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         uint32_t escm = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+          // fast: +0 <= f < V_ESC, one integer compare of the bit pattern (-0, NaN and
+          // (-1, 0) take the exact slow path, which also truncates them to 0)
           const float f = fv[g + q];
           const bool fast = __float_as_uint(f) < 0x49FFC000u;  // bits of (float)V_ESC
           pl[q] = fast ? (uint32_t)f : 0u;
@@ -579,42 +412,52 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           if (full) bad |= sv[g + q] >= S;
         }
         if (__ballot(escm != 0u)) {
-          uint32_t* tmp = stage + threadIdx.x * 8;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            tmp[2 * q] = sv[g + q];
-            tmp[2 * q + 1] = __float_as_uint(fv[g + q]);
-          }
+          // one copy of the full search in the loop's code: slot q picked by selects
 #pragma unroll 1
-          for (int q = 0; q < 4; ++q)
-            if ((escm >> q) & 1u)
-              tmp[2 * q] = pass == 0 ? payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, sumfix)
-                                     : payload1_slow(tmp[2 * q], __uint_as_float(tmp[2 * q + 1]), tb, nullptr);
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if ((escm >> q) & 1u) pl[q] = tmp[2 * q];
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t sq = q == 0 ? sv[g] : q == 1 ? sv[g + 1] : q == 2 ? sv[g + 2] : sv[g + 3];
+            const float fq = q == 0 ? fv[g] : q == 1 ? fv[g + 1] : q == 2 ? fv[g + 2] : fv[g + 3];
+            uint32_t r = 0;
+            if ((escm >> q) & 1u) r = payload1_slow(sq, fq, tb, pass == 0 ? sumfix : nullptr);
+            if ((escm >> q) & 1u) {
+              pl[0] = q == 0 ? r : pl[0];
+              pl[1] = q == 1 ? r : pl[1];
+              pl[2] = q == 2 ? r : pl[2];
+              pl[3] = q == 3 ? r : pl[3];
+            }
+          }
         }
-        uint2 dv[4];
+        uint2 dv[4], lv[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
-        uint32_t bn[4];
+        for (int q = 0; q < 4; ++q) {
+          dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
+          lv[q] = lut2[lut2_index(pl[q])];                      // (used by direct slots only)
+        }
+        uint32_t rc4[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t s = sv[g + q];
           const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);
-          const bool direct = __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
-          rec[h * PH + g + q] = ((s & (ST_TILES * TILE - 1)) << 21) | pl[q];
-          const uint32_t dbin =
-              FS + 2u * (dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw))) + ((s >> 4) & 1u);
-          bn[q] = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+          const bool direct = s < S && __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
+          const uint32_t di = dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw));
+          const uint32_t p = pl[q];
+          uint32_t o;
+          const uint32_t bk = lut2_decode(p, lv[q], o);
+          const bool esc = p >= V_ESC;
+          const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
+          rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
+          const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
+          const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
+          if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
+            const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
+            if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
+              atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
+          }
         }
-        if (!hotrank) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) pk[h * PH + g + q] = atomicAdd(cnt + bn[q], 1u) | (bn[q] << 15);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) pk[h * PH + g + q] = bn[q] << 15;
-        }
+        // slots 4 (kk NT + thread) + q of this group kk, as loaded
+        *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4) * NT + threadIdx.x)) =
+            make_uint4(rc4[0], rc4[1], rc4[2], rc4[3]);
         asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
       }
     }
@@ -683,7 +526,13 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         r += c[q] ? 1u : 0u;
       }
     }
-    __syncthreads();  // B2: offsets, run ranks, heads
+    uint32_t rec[PT];  // this thread's records, in slot order (read before any is scattered)
+#pragma unroll
+    for (int kk = 0; kk < PT / 4; ++kk) {
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + 4u * ((uint32_t)kk * NT + threadIdx.x));
+      rec[4 * kk] = v.x; rec[4 * kk + 1] = v.y; rec[4 * kk + 2] = v.z; rec[4 * kk + 3] = v.w;
+    }
+    __syncthreads();  // B2: offsets, run ranks, heads; every slot-order record read
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = pk[k] >> 15;
@@ -711,6 +560,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B3: stage, group prefixes, deltas (every count read: cleared below)
+    const uint32_t nst = offr[FS] >> 16;  // runs of super-tile bins (u32 records); the later runs are u16
 #pragma unroll
     for (int j = 0; j < RB; ++j)
       if (threadIdx.x + (uint32_t)j * NT < BIN1_BINS) cnt[threadIdx.x + (uint32_t)j * NT] = 0;
@@ -721,20 +571,31 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
-#if defined(L5DH_EXP) && (L5DH_EXP & 32)  // timing only: the same records written sequentially
-      if (d != INVALID) rec32[c0 + i] = stage[i];
-#else
-      if (d != INVALID) rec32[i + d] = stage[i];
-#endif
+      if (d != INVALID) {
+        if (run < nst)
+          rec32[i + d] = stage[i];
+        else
+          rec16[i + d] = (uint16_t)stage[i];
+      }
     }
     __syncthreads();  // B4
   }
-  if (pass == 0 && bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
+  if (pass == 0) {
+    // the slab's direct value sums (every wave's adds are in: the last barrier) into sumfix
+    const uint32_t* dl = meta + L.dlist();
+    for (uint32_t i = threadIdx.x; i < ND * TILE; i += NT) {
+      const uint32_t v = dsum[i];
+      const uint32_t s = dl[i / TILE] * TILE + (i & (TILE - 1));
+      if (v && s < S) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)v);
+    }
+    if (bad) atomicAdd(err, 1u);  // monotonic: the host compares it with the count it already reported
+  }
 }
 
 // ------------------------------------------------------------------------
 // After level 1 (one workgroup, thread = bin): exact bin totals, the direct keys'
-// ranges, and on an overflow exact regions for the redo pass.
+// ranges, and on an overflow exact regions for the redo pass (super-tile bins in
+// rec32, direct half-bins in rec16 from 0; H_D16 = their total).
 __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict__ meta, const uint32_t* __restrict__ err,
                                                 uint32_t* __restrict__ err_host) {
   __shared__ uint32_t lds[17];
@@ -746,26 +607,32 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
   const uint32_t TB = FS + 2 * ND;
   const uint32_t ov = hdr[H_OV1];
   const uint32_t b = threadIdx.x;
+  const bool stb = b < FS, dj = b >= FS && b < TB;
   const uint32_t c = b < TB ? meta[L.bcnt() + b] : 0u;
   meta[L.btot() + b] = c;
-  uint32_t tot;
-  const uint32_t nb = block_excl_scan<1024>(round_up(c, 4), lds, &tot);
+  uint32_t t32, t16;
+  const uint32_t nb32 = block_excl_scan<1024>(stb ? round_up(c, 4) : 0u, lds, &t32);
+  const uint32_t nb16 = block_excl_scan<1024>(dj ? round_up(c, 8) : 0u, lds, &t16);
+  const uint32_t nb = stb ? nb32 : nb16;
   const uint32_t base = ov ? nb : meta[L.bbase() + b];
-  if (b >= FS && b < TB) {
+  if (dj) {
     const uint32_t t = meta[L.dlist() + ((b - FS) >> 1)], h = (b - FS) & 1u;
     meta[L.kbase() + 2 * t + h] = base;
     meta[L.kcnt() + 2 * t + h] = c;
   }
   if (ov) {
     meta[L.bbase() + b] = nb;
-    meta[L.bcap() + b] = round_up(c, 4);
+    meta[L.bcap() + b] = round_up(c, stb ? 4 : 8);
     meta[L.bcnt() + b] = 0u;
   }
   __syncthreads();  // every thread has read H_OV1
   if (b == 0) {
     hdr[H_REDO1] = ov;
     hdr[H_OV1] = 0u;
-    if (ov) hdr[H_NOVR1] += 1u;
+    if (ov) {
+      hdr[H_NOVR1] += 1u;
+      hdr[H_D16] = t16;
+    }
   }
 }
 
@@ -830,7 +697,8 @@ __global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restri
   const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
   uint32_t cap = mine ? meta[L.kcap() + k] : 0u;
   uint64_t total;
-  const uint64_t base = before + block_excl_scan64((uint64_t)cap, l64, &total);
+  // (level-2 regions follow the direct keys' regions of rec16)
+  const uint64_t base = hdr[H_D16] + before + block_excl_scan64((uint64_t)cap, l64, &total);
   if (mine) {
     if (base + cap + 64 > cap16) cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
     meta[L.kbase() + k] = (uint32_t)base;
@@ -1096,7 +964,7 @@ __global__ __launch_bounds__(1024) void k_rfix2b(uint32_t F, uint32_t* __restric
   const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
   const uint32_t c8 = mine ? round_up(meta[L.kcnt() + k], 8) : 0u;
   uint64_t total;
-  const uint64_t base = before + block_excl_scan64((uint64_t)c8, l64, &total);
+  const uint64_t base = hdr[H_D16] + before + block_excl_scan64((uint64_t)c8, l64, &total);
   if (mine) {
     meta[L.kbase() + k] = (uint32_t)base;
     meta[L.kcap() + k] = c8;
@@ -1121,8 +989,6 @@ __global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__
   }
 }
 
-constexpr int CH1 = 16384;
-
 }  // namespace
 
 hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
@@ -1139,15 +1005,8 @@ hipError_t set_ingest_attributes() {
     return e;
   if ((e = hipFuncSetAttribute((const void*)k_rplan1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RPLAN1_LDS)))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_rbin1<CH1, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1_lds(CH1))))
-    return e;
-  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<768, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds(CHW))) ||
-      (e = hipFuncSetAttribute((const void*)k_rbin1w<512, 8192>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds(8192))) ||
-      (e = hipFuncSetAttribute((const void*)k_rbin1w<1024, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds(CHW))))
+  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<NT1, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)rbin1w_lds())))
     return e;
   return hipFuncSetAttribute((const void*)k_rbin2<B2_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
 }
@@ -1159,32 +1018,12 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
       hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
                          a.kest);
       hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
-                         a.thr_min, a.dmax, a.pct);
+                         a.dlim16, a.thr_min, a.dmax, a.pct);
       break;
     case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
       for (int pass = 0; pass < 2; ++pass) {
-        switch (a.l1) {
-          case 1:
-            hipLaunchKernelGGL((k_rbin1<CH1, 1024>), dim3(a.G), dim3(1024), rbin1_lds(CH1), st, a.series, a.values,
-                               a.n, a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
-            break;
-          case 2: {  // 8K-slot sub-chunks, two 512-thread workgroups per CU (twice the slabs)
-            const size_t G2 = std::min<size_t>(2 * (size_t)a.G, (a.n + 8191) / 8192);
-            size_t per2 = ((a.n + G2 - 1) / G2 + 3) & ~(size_t)3;
-            const size_t g2 = (a.n + per2 - 1) / per2;
-            hipLaunchKernelGGL((k_rbin1w<512, 8192>), dim3((unsigned)std::max<size_t>(g2, 1)), dim3(512),
-                               rbin1w_lds(8192), st, a.series, a.values, a.n, per2, a.S, a.F, a.tb, a.meta, a.rec32,
-                               a.sumfix, a.err, a.vec ? 1 : 0, pass);
-            break;
-          }
-          case 3:
-            hipLaunchKernelGGL((k_rbin1w<1024, CHW>), dim3(a.G), dim3(1024), rbin1w_lds(CHW), st, a.series, a.values,
-                               a.n, a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
-            break;
-          default:
-            hipLaunchKernelGGL((k_rbin1w<768, CHW>), dim3(a.G), dim3(768), rbin1w_lds(CHW), st, a.series, a.values, a.n,
-                               a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.sumfix, a.err, a.vec ? 1 : 0, pass);
-        }
+        hipLaunchKernelGGL((k_rbin1w<NT1, CHW>), dim3(a.G), dim3(NT1), rbin1w_lds(), st, a.series, a.values, a.n,
+                           a.per, a.S, a.F, a.tb, a.meta, a.rec32, a.rec16, a.sumfix, a.err, a.vec ? 1 : 0, pass);
         if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);
       }
       break;

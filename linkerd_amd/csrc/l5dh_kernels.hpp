@@ -20,24 +20,26 @@ constexpr int ST_SHIFT = 11;        // 64 tiles x 32 series
 constexpr int ROW = 1800;           // state row stride in u32 (16-B aligned rows)
 constexpr int CROW = 900;           // u16-packed cold row in LDS, in u32 words
 constexpr int HROW = 1800;          // u32 hot row in LDS
-// Level-1 record (u32, rec32):
+// Level-1 record of a super-tile bin (u32, rec32):
 //   [31:26] tile in super-tile | [25:21] series in tile | [20:0] payload,
 //   payload = v = (long)sample when 0 <= v < V_ESC, else V_ESC + bucket (the
 //   sample's exact contribution to `total` went to sumfix[series]).
-// Level-2 record (u16, rec16): [15:11] series in tile | [10:0] bucket; the value
-//   sums of level-2 records are folded into sumfix by k_rbin2.
+// Final record (u16, rec16): [15:11] series in tile | [10:0] bucket.  Level 1 writes
+//   them for the direct tiles (bucketized there, value sums folded in LDS into
+//   sumfix), level 2 for the other tiles (value sums folded per super-tile).
 constexpr uint32_t V_ESC = (1u << 21) - 2048u;
 constexpr int MAX_SEG = 8;
 constexpr int WG = 1024;            // threads per workgroup of the heavy kernels
 constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow below this
 
-// LDS bytes of the accumulate kernels: 32 u16-packed rows (cold tiles) or 16 u32
-// rows (big half-tiles), lane-private value sums, the bucket LUT
-constexpr size_t acc_cold_lds(int nser) { return (size_t)nser * CROW * 4 + nser * 64 * 4 + 1024 * 8 + nser * 8 + 16; }
-constexpr size_t acc_cold_p_lds(int nser) { return acc_cold_lds(nser) + ROW * 4; }  // + bucket midpoints
-// big half-tile: 16 u32 rows, 16 x 64 lane-private u64 value sums, the bucket LUT
-constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
-constexpr size_t ACC_HOT_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 8 + 1024 * 8;  // u16 bins of 32 series, u64 sums
+// LDS bytes of the accumulate kernels: 32 u16-packed rows + the tile's sumfix + the
+// bucket midpoints (cold tiles), 16 u32 rows (big half-tiles)
+constexpr size_t ACC_COLD_LDS = (size_t)TILE * CROW * 4 + TILE * 8 + ROW * 4;
+constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4;
+// k_fold1 (samples, not records): u32 rows of 16 series or u16-packed rows of 32, lane-private
+// u64 value sums, the bucket LUT
+constexpr size_t FOLD16_LDS = (size_t)16 * HROW * 4 + 16 * 64 * 8 + 1024 * 8;
+constexpr size_t FOLD32_LDS = (size_t)TILE * CROW * 4 + TILE * 64 * 8 + 1024 * 8;
 
 constexpr int LUT_N = 1664;         // bucket bracket LUT: 64 direct + 25 octaves x 64
 constexpr int LUT2_N = 1024;        // exact bucket + offset LUT for keys < 2^21 (64 direct + 15 octaves x 64)
@@ -51,9 +53,9 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 };
 
 // ---- binned segments (one ingest batch each) -------------------------------
-// Every (tile, half) "key" k = 2 t + h of a segment is ONE contiguous range of
-// records: [kbase[k], kbase[k] + kcnt[k]) of rec32 when tile t is a direct tile of
-// the batch (its records were written by level 1), of rec16 otherwise (level 2).
+// Every (tile, half) "key" k = 2 t + h of a segment is ONE contiguous range of u16
+// records: [kbase[k], kbase[k] + kcnt[k]) of rec16 -- written by level 1 when tile
+// t is a direct tile of the batch (regions [0, H_D16)), by level 2 otherwise.
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
@@ -89,12 +91,12 @@ enum : uint32_t {
   H_HS = 8,       // 1: one bin holds >= half the batch
   H_EXACT = 9,    // 1: every sample of the batch was counted by k_rsample
   H_NOVR1 = 10,   // level-1 redos (diagnostics, monotonic per segment slot)
-  H_NOVR2 = 11
+  H_NOVR2 = 11,
+  H_D16 = 12      // rec16 records reserved for the direct keys' regions (level-2 regions follow)
 };
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 
 struct Segs {              // binned ingest batches awaiting aggregation
-  const uint32_t* rec32[MAX_SEG];
   const uint16_t* rec16[MAX_SEG];
   const uint32_t* meta[MAX_SEG];
   int n;
@@ -115,7 +117,6 @@ struct State {
 };
 
 constexpr uint32_t CI_DIRTY = 1u << 30;  // cold item: the tile held live counts
-constexpr uint32_t CI_R32 = 1u << 31;    // cold item: its records are rec32 (a direct tile)
 constexpr uint8_t TF_SPLIT = 2;    // big tile, accumulated per half
 constexpr uint8_t TF_DIRTY = 4;    // the tile held live counts when k_plan ran
 constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, each half ONE item:
@@ -123,8 +124,8 @@ constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, 
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
-  uint4* cold_item;        // [F] cold item -> {tile | CI_DIRTY | CI_R32, a0, a1, n0 | n1 << 16}: segment 0's
-                           // key ranges of the tile's halves (rec32 records when CI_R32, else rec16)
+  uint4* cold_item;        // [F] cold item -> {tile | CI_DIRTY, a0, a1, n0 | n1 << 16}: segment 0's
+                           // key ranges (rec16) of the tile's halves
   uint2* split_item;       // [split items] {tile | half << 15, chunk} of big tiles
   uint32_t* hot_list;      // [F] big tiles
   uint8_t* tile_flags;     // [F] TF_*
@@ -159,11 +160,10 @@ struct IngestArgs {
   uint32_t* rec32;         // [cap32]
   uint16_t* rec16;         // [cap16]
   size_t cap32, cap16;
+  size_t dlim16;           // rec16 records the direct keys' regions may take ([0, dlim16); level 2 gets the rest)
   uint32_t thr_min, dmax;  // direct tiles: >= thr_min estimated records, at most dmax of them
   uint32_t pct;            // region capacity scale, percent (100: as predicted)
   bool vec;                // 16-B aligned inputs
-  int l1;                  // level-1 kernel: 0 k_rbin1w<768> (24K-slot sub-chunks), 1 k_rbin1 (16K),
-                           // 2 k_rbin1w<512> (8K slots, 2 per CU), 3 k_rbin1w<1024> (L5DH_PARAM_VARIANT bits 3:2)
 };
 // Stages: 0 = sample + level-1 plan + level 1 (+ redo), 1 = level-2 plan + level 2 (+ redo).
 hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st);
@@ -187,7 +187,7 @@ constexpr uint32_t DEV_COUNT = 0xFFFFFFFFu;
 // instead of their state rows, and k_hot_finish summarizes them in place.
 hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out, int direct_out, hipStream_t st);
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
-                             int final_mode, int reset, int stores_first, hipStream_t st);
+                             int final_mode, int reset, hipStream_t st);
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
                               Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,

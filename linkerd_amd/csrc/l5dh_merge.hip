@@ -15,6 +15,8 @@
 //   k_mdecode  summed rows of this rank's slice from every source + HistogramSummary
 //   k_scan_*   u32 word counts -> u64 exclusive offsets (tile sums, one-workgroup
 //              scan of the tile sums, tile scans)
+#include <algorithm>
+
 #include "l5dh_device.hpp"
 #include "l5dh_merge.hpp"
 
@@ -202,7 +204,41 @@ hipError_t exclusive_scan_u32_u64(const uint32_t* x, uint32_t n, uint64_t* out, 
 
 size_t scan_tmp_bytes(uint32_t n) { return ((size_t)n / SCAN_TILE + 2) * 8; }
 
+// The loopback transport's reductions: element-wise sums over the group's buffers.
+template <class T>
+struct SrcList {
+  const T* p[MERGE_MAX_RANKS];
+  int n;
+};
+template <class T>
+__global__ __launch_bounds__(256) void k_loop_sum(SrcList<T> src, T* __restrict__ dst, size_t count) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+    T acc = 0;
+    for (int k = 0; k < src.n; ++k) acc += src.p[k][i];
+    dst[i] = acc;
+  }
+}
+template <class T>
+hipError_t loop_sum(const T* const* srcs, int n, T* dst, size_t count, hipStream_t st) {
+  if (count == 0) return hipSuccess;
+  if (n < 1 || n > MERGE_MAX_RANKS) return hipErrorInvalidValue;
+  SrcList<T> l{};
+  for (int k = 0; k < n; ++k) l.p[k] = srcs[k];
+  l.n = n;
+  const size_t blocks = std::min<size_t>((count + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_loop_sum<T>, dim3((unsigned)blocks), dim3(256), 0, st, l, dst, count);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t merge_loop_sum_i32(const int32_t* const* srcs, int n, int32_t* dst, size_t count, hipStream_t st) {
+  return loop_sum(srcs, n, dst, count, st);
+}
+hipError_t merge_loop_sum_i64(const int64_t* const* srcs, int n, int64_t* dst, size_t count, hipStream_t st) {
+  return loop_sum(srcs, n, dst, count, st);
+}
 
 hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
                        size_t* tmp_bytes, hipStream_t st) {

@@ -23,6 +23,9 @@ hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* off
 // offs[0..nrows) = exclusive prefix of words (a received slice); tmp from merge_count's query
 hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
                          hipStream_t st);
+// dst[i] = sum over k < n of srcs[k][i] (the loopback transport's reductions; dst may be srcs[0])
+hipError_t merge_loop_sum_i32(const int32_t* const* srcs, int n, int32_t* dst, size_t count, hipStream_t st);
+hipError_t merge_loop_sum_i64(const int64_t* const* srcs, int n, int64_t* dst, size_t count, hipStream_t st);
 // summed rows of the slice (out_rows nullable: [nrows][1798]) and their summaries
 hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
                         Summary88* out_summ, hipStream_t st);

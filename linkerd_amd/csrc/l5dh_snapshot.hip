@@ -11,9 +11,8 @@
 //   k_rows         summaries / dense copies of state rows or external rows
 //   k_fold1        one-tile series spaces folded into state rows at ingest
 //
-// Every (tile, half) key of a segment is one contiguous range (l5dh_kernels.hpp):
-// rec32 level-1 records of a direct tile (payload: value or escaped bucket), or
-// rec16 level-2 records (series in tile | bucket; their value sums are in sumfix).
+// Every (tile, half) key of a segment is one contiguous range of rec16 records
+// (l5dh_kernels.hpp: series in tile | bucket; their value sums are in sumfix).
 #include "l5dh_device.hpp"
 
 namespace l5dh {
@@ -21,8 +20,7 @@ namespace {
 
 // Records of key (t, h) in segment j.
 struct KeyRange {
-  const uint32_t* r32;  // non-null: rec32 records
-  const uint16_t* r16;  // else rec16 records
+  const uint16_t* r16;
   uint32_t a, e;
 };
 __device__ __forceinline__ KeyRange seg_key(const Segs& sg, int j, uint32_t F, uint32_t t, uint32_t h) {
@@ -30,8 +28,7 @@ __device__ __forceinline__ KeyRange seg_key(const Segs& sg, int j, uint32_t F, u
   const uint32_t* m = sg.meta[j];
   const uint32_t k = 2 * t + h;
   const uint32_t a = m[L.kbase() + k], c = m[L.kcnt() + k];
-  const bool d = (m[L.dbits() + (t >> 5)] >> (t & 31u)) & 1u;
-  return KeyRange{d ? sg.rec32[j] : nullptr, d ? nullptr : sg.rec16[j], a, a + c};
+  return KeyRange{sg.rec16[j], a, a + c};
 }
 __device__ __forceinline__ uint32_t seg_key_count(const Segs& sg, int j, uint32_t F, uint32_t k) {
   return sg.meta[j][meta_layout(F).kcnt() + k];
@@ -155,7 +152,6 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
       uint4 ci = make_uint4(t | (dirty[t] ? CI_DIRTY : 0u), 0u, 0u, 0u);
       if (segs.n > 0) {  // segment 0's key ranges (the cold kernel prefetches them with one load)
         const KeyRange r0 = seg_key(segs, 0, F, t, 0), r1 = seg_key(segs, 0, F, t, 1);
-        ci.x |= r0.r32 ? CI_R32 : 0u;
         ci.y = r0.a;
         ci.z = r1.a;
         ci.w = (r0.e - r0.a) | ((r1.e - r1.a) << 16);
@@ -323,59 +319,37 @@ __device__ __forceinline__ void count16(uint4 x, uint32_t m, Hist&& hist_add) {
 
 // The records of both halves of tile t in every segment: per segment, the two
 // ranges are walked together (a thread's loads of both halves in flight at once).
-// Ranges start 16-B aligned (rec32 regions at multiples of 4, rec16 of 8).
-template <int NT, class Hist, class Sum>
-__device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t t, const uint2* __restrict__ lut2,
-                                           Hist&& hist_add, Sum&& sum_add) {
+// Ranges start 16-B aligned (rec16 regions at multiples of 8).
+template <int NT, class Hist>
+__device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t t, Hist&& hist_add) {
   for (int j = 0; j < sg.n; ++j) {
     const KeyRange r0 = seg_key(sg, j, F, t, 0), r1 = seg_key(sg, j, F, t, 1);
-    if (r0.r32) {
-      const uint32_t n0 = r0.e - r0.a, n1 = r1.e - r1.a;
-      const uint32_t g0 = (n0 + 3) / 4, g1 = (n1 + 3) / 4, gm = max(g0, g1);
-      const uint4* p0 = reinterpret_cast<const uint4*>(r0.r32 + r0.a);
-      const uint4* p1 = reinterpret_cast<const uint4*>(r1.r32 + r1.a);
-      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
-        const uint4 x = g < g0 ? p0[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
-        const uint4 y = g < g1 ? p1[g] : make_uint4(~0u, ~0u, ~0u, ~0u);
-        uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (4 * g + k >= n0) v[k] = 0xFFFFFFFFu;
-          if (4 * g + k >= n1) v[4 + k] = 0xFFFFFFFFu;
-        }
-        count_batch<8>(v, lut2, hist_add, sum_add);
-      }
-    } else {
-      const uint32_t n0 = r0.e - r0.a, n1 = r1.e - r1.a;
-      const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
-      const uint4* p0 = reinterpret_cast<const uint4*>(r0.r16 + r0.a);
-      const uint4* p1 = reinterpret_cast<const uint4*>(r1.r16 + r1.a);
-      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
-        const uint4 x = g < g0 ? p0[g] : make_uint4(0u, 0u, 0u, 0u);
-        const uint4 y = g < g1 ? p1[g] : make_uint4(0u, 0u, 0u, 0u);
-        count16(x, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
-        count16(y, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
-      }
+    const uint32_t n0 = r0.e - r0.a, n1 = r1.e - r1.a;
+    const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
+    const uint4* p0 = reinterpret_cast<const uint4*>(r0.r16 + r0.a);
+    const uint4* p1 = reinterpret_cast<const uint4*>(r1.r16 + r1.a);
+    for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+      const uint4 x = g < g0 ? p0[g] : make_uint4(0u, 0u, 0u, 0u);
+      const uint4 y = g < g1 ? p1[g] : make_uint4(0u, 0u, 0u, 0u);
+      count16(x, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
+      count16(y, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
     }
   }
 }
 
 // k_accum_cold_p: one 1024-thread workgroup per CU walks the cold tiles (<= 65535
-// records: u16 bins cannot overflow) blockIdx.x, + gridDim.x, ...: 32 series in
-// u16-packed LDS bins, lane-private u32 value sums of the level-1 records, then one
-// wave per series emits the dense row and the summary.  The LUT and the midpoints
-// are staged once; each wave clears its series' LDS rows right after emitting them.
+// records: u16 bins cannot overflow): 32 series in u16-packed LDS bins, then one wave
+// per series emits the dense row and the summary (the series' exact sum is its
+// sumfix: the value sums were folded at ingest).  The midpoints are staged once;
+// each wave clears its series' LDS rows right after emitting them.
 __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                          uint32_t cold_arg, int final_mode, int reset,
-                                                          int stores_first) {
+                                                          uint32_t cold_arg, int final_mode, int reset) {
   constexpr int NT = 1024;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t cold_items = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
-  uint32_t* hist = smem;                                      // [32][900] u16 pairs
-  uint32_t* vsl = smem + TILE * CROW;                         // [32][64] lane-private value sums
-  uint2* lut2 = reinterpret_cast<uint2*>(vsl + TILE * 64);    // [LUT2_N]
-  int64_t* fixl = reinterpret_cast<int64_t*>(lut2 + LUT2_N);  // [32] sumfix of the item's series
-  int32_t* midl = reinterpret_cast<int32_t*>(fixl + TILE);    // [NB] bucket midpoints (the summary's lookups)
+  uint32_t* hist = smem;                                        // [32][900] u16 pairs
+  int64_t* fixl = reinterpret_cast<int64_t*>(smem + TILE * CROW);  // [32] sumfix of the item's series
+  int32_t* midl = reinterpret_cast<int32_t*>(fixl + TILE);      // [NB] bucket midpoints (the summary's lookups)
   const int w = threadIdx.x >> 6;
   const int lane = lane_id();
   const bool keep = !(final_mode && reset);
@@ -385,12 +359,9 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   auto hist_add = [&](uint32_t loc, uint32_t b) {
     atomicAdd(&hist[(loc & 31u) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
   };
-  // (a slot gathers <= 65535 / 64 records of one lane of ONE wave per tile: < 2^32)
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 31u) * 64 + lane], v); };
   {
     uint4* p = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < (TILE * CROW + TILE * 64) / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+    for (int i = threadIdx.x; i < TILE * CROW / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
   }
   // The next item is fetched during this item's emission (its latency hides behind the
@@ -400,11 +371,10 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   // it is placed before the emission.
   const bool one = segs.n == 1;
   uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0;
-  bool dirty = false, r32 = false;
+  bool dirty = false;
   int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
-  const char* const b32 = reinterpret_cast<const char*>(segs.rec32[0]);
-  const char* const b16 = reinterpret_cast<const char*>(segs.rec16[0]);
+  const uint16_t* const b16 = segs.rec16[0];
   auto fetch = [&](uint4 ci) {
     // (the entry stays in VGPRs until here, where it becomes scalars: converted at its
     // load, it would be waited for there)
@@ -412,17 +382,14 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t cx = __builtin_amdgcn_readfirstlane(ci.x), cw = __builtin_amdgcn_readfirstlane(ci.w);
     t = cx & 0x7FFFu;
     dirty = (cx & CI_DIRTY) != 0u;
-    r32 = (cx & CI_R32) != 0u;
     a0 = __builtin_amdgcn_readfirstlane(ci.y);
     a1 = __builtin_amdgcn_readfirstlane(ci.z);
     n0 = cw & 0xFFFFu;
     n1 = cw >> 16;
     if (one) {
       const uint32_t g = threadIdx.x;
-      const uint32_t per = r32 ? 4u : 8u, esz = r32 ? 4u : 2u;
-      const char* base = r32 ? b32 : b16;
-      x0 = *reinterpret_cast<const uint4*>(base + (size_t)esz * (per * g < n0 ? a0 + per * g : a0));
-      x1 = *reinterpret_cast<const uint4*>(base + (size_t)esz * (per * g < n1 ? a1 + per * g : a1));
+      x0 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n0 ? a0 + 8 * g : a0));
+      x1 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n1 ? a1 + 8 * g : a1));
     }
     fraw = st.sumfix[min(t * TILE + (threadIdx.x & (TILE - 1)), st.S - 1)];
   };
@@ -435,11 +402,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   __shared__ uint32_t s_next[2];
   uint32_t* const ctr = plan.header + 2;  // zeroed by k_plan_b
   const uint32_t G2 = 2u * gridDim.x;
-#if defined(L5DH_EXP) && (L5DH_EXP & 64)
-  if (threadIdx.x == 0) s_next[0] = blockIdx.x + G2;
-#else
   if (threadIdx.x == 0) s_next[0] = G2 + atomicAdd(ctr, 1u);
-#endif
   uint32_t item = blockIdx.x, item1 = blockIdx.x + gridDim.x;
   if (item < cold_items) fetch(citem[item]);
   uint4 cn = citem[min(item1, last)];  // the next item's entry, in flight
@@ -455,50 +418,27 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     }
     if (one) {
       // group g of both halves: the prefetched first one, then g + NT, ...
-      if (r32) {
-        const uint32_t g0 = (n0 + 3) / 4, g1 = (n1 + 3) / 4, gm = max(g0, g1);
-        const uint4* p0 = reinterpret_cast<const uint4*>(segs.rec32[0] + a0);
-        const uint4* p1 = reinterpret_cast<const uint4*>(segs.rec32[0] + a1);
-        uint4 x = x0, y = x1;
-        for (uint32_t g = threadIdx.x; g < gm; g += NT) {
-          uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (4 * g + k >= n0) v[k] = 0xFFFFFFFFu;
-            if (4 * g + k >= n1) v[4 + k] = 0xFFFFFFFFu;
-          }
-          const uint32_t gn = g + NT;
-          x = gn < g0 ? p0[gn] : make_uint4(~0u, ~0u, ~0u, ~0u);
-          y = gn < g1 ? p1[gn] : make_uint4(~0u, ~0u, ~0u, ~0u);
-          count_batch<8>(v, lut2, hist_add, sum_add);
-        }
-      } else {
-        const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
-        const uint4* p0 = reinterpret_cast<const uint4*>(segs.rec16[0] + a0);
-        const uint4* p1 = reinterpret_cast<const uint4*>(segs.rec16[0] + a1);
-        uint4 x = x0, y = x1;
-        for (uint32_t g = threadIdx.x; g < gm; g += NT) {
-          const uint4 cx = x, cy = y;
-          const uint32_t gn = g + NT;
-          x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
-          y = gn < g1 ? p1[gn] : make_uint4(0u, 0u, 0u, 0u);
-          count16(cx, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
-          count16(cy, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
-        }
+      const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
+      const uint4* p0 = reinterpret_cast<const uint4*>(b16 + a0);
+      const uint4* p1 = reinterpret_cast<const uint4*>(b16 + a1);
+      uint4 x = x0, y = x1;
+      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
+        const uint4 cx = x, cy = y;
+        const uint32_t gn = g + NT;
+        x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
+        y = gn < g1 ? p1[gn] : make_uint4(0u, 0u, 0u, 0u);
+        count16(cx, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
+        count16(cy, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
       }
     } else {
-      count_tile<NT>(segs, F, tc, lut2, hist_add, sum_add);
+      count_tile<NT>(segs, F, tc, hist_add);
     }
     __syncthreads();  // counts complete; fixl visible
     fetch(cn);  // (past the last item: a harmless refetch of the last entry)
     const uint32_t item2 = s_next[par];
     cn = citem[min(item2, last)];
     uint32_t asked = 0;
-#if defined(L5DH_EXP) && (L5DH_EXP & 64)
-    if (threadIdx.x == 0) asked = item2 + gridDim.x;
-#else
     if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);  // (stored at the end of the emission)
-#endif
     const uint32_t s0 = tc * TILE;
     // linear emission: a clean whole tile inside the output range of a resetting
     // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
@@ -507,34 +447,10 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
                         s0 + TILE <= st.S && (oi0 & 1u) == 0u;
-    // linear: the summaries, then the 32 rows' stores as one range (chunk c = flat
-    // elements 4c..4c+3 of [32][1798]: two u16 pairs), each clearing the words it read.
-    // (stores_first, variant bit 4: the stores issued before the summaries and the rows
-    // cleared after both -- measured slower, accum 2.40 vs 2.28 ms, profiles/r03n_ab_16.log)
-    auto linear_stores = [&](bool clear) {
-      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
-      constexpr int NCH = TILE * NB / 4;
-      for (int c = threadIdx.x; c < NCH; c += NT) {
-        const int e0 = 4 * c;
-        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
-        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
-        // the second pair is the next word (one ds_read2), except for the chunk that
-        // straddles into the next row (b0 = 1796; word 899 of a row is never written)
-        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
-        const uint32_t x = *p0, y = *p1;
-        if (clear) {
-          *p0 = 0u;
-          *p1 = 0u;
-        }
-        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
-      }
-    };
-    if (linear && stores_first) linear_stores(false);
     for (int loc = w; loc < TILE; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
-        const uint64_t vsum = wave_sum((uint64_t)vsl[loc * 64 + lane]);
         if (linear) {
           const int ng = lane_groups(lane);
           uint32_t g[9], nw = 0;
@@ -548,25 +464,34 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
             }
           }
           put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
-          wave_summary(g, SrcLds16{row}, (int64_t)vsum + fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
-          if (lane == 0 && out.totals) out.totals[s - out.first] = (int64_t)vsum + fixl[loc];
+          wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
         } else {
-          emit_series(SrcLds16{row}, s, vsum, fixl[loc], dc, keep, final_mode, st, tbl, out);
+          emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
         }
       }
       if (!linear) {  // this wave owns the row: clear it for the next item (a wave's LDS ops stay in order)
         uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
         for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
       }
-      vsl[loc * 64 + lane] = 0u;
     }
     if (linear) {
-      __syncthreads();  // the stores and the summaries have read the rows
-      if (stores_first) {
-        uint4* hp = reinterpret_cast<uint4*>(hist);
-        for (int i = threadIdx.x; i < TILE * CROW / 4; i += NT) hp[i] = make_uint4(0u, 0u, 0u, 0u);
-      } else {
-        linear_stores(true);
+      __syncthreads();  // the summaries have read the rows
+      // the 32 rows' stores as one range (chunk c = flat elements 4c..4c+3 of
+      // [32][1798]: two u16 pairs), each clearing the words it read
+      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
+      constexpr int NCH = TILE * NB / 4;
+      for (int c = threadIdx.x; c < NCH; c += NT) {
+        const int e0 = 4 * c;
+        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
+        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
+        // the second pair is the next word (one ds_read2), except for the chunk that
+        // straddles into the next row (b0 = 1796; word 899 of a row is never written)
+        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
+        const uint32_t x = *p0, y = *p1;
+        *p0 = 0u;
+        *p1 = 0u;
+        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
       }
     }
     if (threadIdx.x == 0) {
@@ -707,9 +632,8 @@ __global__ __launch_bounds__(WG) void k_fold1(const uint32_t* __restrict__ serie
 
 // Big tiles: item = (tile, half, chunk of hot_chunk records of that half across the
 // pending segments; each segment holds the half as one contiguous range).  u32 LDS
-// bins for the half's 16 series, lane-private u64 value sums of the level-1 records,
-// flushed with global atomics (k_hot_init cleared the rows; k_hot_finish
-// summarizes them).
+// bins for the half's 16 series, flushed with global atomics (k_hot_init cleared the
+// rows; k_hot_finish summarizes them); the exact sums are already in sumfix.
 __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                     int direct_out, uint32_t hot_chunk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -717,12 +641,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   const uint32_t F = st.F;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
-  uint32_t* hist = smem;                                                              // [16][1800]
-  unsigned long long* vsl = reinterpret_cast<unsigned long long*>(smem + 16 * HROW);  // [16][64]
-  uint2* lut2 = reinterpret_cast<uint2*>(smem + 16 * HROW + 16 * 64 * 2);             // [LUT2_N]
-  for (int i = threadIdx.x; i < LUT2_N; i += WG) lut2[i] = tb.lut2[i];
+  uint32_t* hist = smem;  // [16][1800]
   auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); };
-  auto sum_add = [&](uint32_t loc, uint32_t v) { atomicAdd(&vsl[(loc & 15u) * 64 + lane], (unsigned long long)v); };
   // items: blockIdx.x first, then from a counter (G, G + 1, ...) as workgroups finish
   __shared__ uint32_t s_item;
   uint32_t* const ctr = plan.header + 4 + 3 * ((F + 1023) / 1024);  // zeroed by k_plan_b
@@ -731,7 +651,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
     const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
     {
       uint4* q = reinterpret_cast<uint4*>(smem);
-      for (int i = threadIdx.x; i < (16 * HROW + 16 * 64 * 2) / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < 16 * HROW / 4; i += WG) q[i] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const uint64_t vlo = (uint64_t)it.y * hot_chunk, vhi = vlo + hot_chunk;
@@ -749,24 +669,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       // loads are unconditional (a group past the range reloads the first one; records
       // outside [a, e) are masked where they are used), so the next groups stay in flight
       // while this one is counted
-      if (r.r32) {
-        const uint32_t a4 = a & ~3u;
-        auto ld = [&](uint32_t g) { return *reinterpret_cast<const uint4*>(r.r32 + (g < e ? g : a4)); };
-        uint32_t g = a4 + 4u * threadIdx.x;
-        uint4 n0 = ld(g), n1 = ld(g + 4u * WG);
-        for (uint32_t c = a4; c < e; c += 8u * WG, g += 8u * WG) {
-          const uint4 x0 = n0, x1 = n1;
-          n0 = ld(g + 8u * WG);
-          n1 = ld(g + 12u * WG);
-          uint32_t x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t gk = g + (k >> 2) * 4u * WG + (k & 3);
-            if (gk < a || gk >= e) x[k] = 0xFFFFFFFFu;
-          }
-          count_batch<8>(x, lut2, hist_add, sum_add);
-        }
-      } else {
+      {
         const uint32_t a8 = a & ~7u;
         auto ld = [&](uint32_t g) { return *reinterpret_cast<const uint4*>(r.r16 + (g < e ? g : a8)); };
         uint32_t g = a8 + 8u * threadIdx.x;
@@ -792,14 +695,13 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       }
     }
     __syncthreads();
-    const uint64_t my_vsum = wave_sum((uint64_t)vsl[w * 64 + lane]);
     const uint32_t s = t * TILE + 16 * half + w;
     if (plan.tile_flags[t] & TF_SOLO) {
       // this item holds every record of the half: wave w writes series w's output row,
       // total and summary (direct_out: out.first == 0, the tile is clean, reset)
       if (s < st.S) {
         const SrcLds32 src{hist + w * HROW};
-        const int64_t total = (int64_t)my_vsum + st.sumfix[s];
+        const int64_t total = st.sumfix[s];
         uint32_t g[9];
         row_pass(src, g, out.counts + (size_t)s * NB, out.words ? out.words + s : nullptr);
         wave_summary(g, src, total, tb.mid, out.summ ? out.summ + s : nullptr);
@@ -821,13 +723,8 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
           if (v) atomicAdd(&grow[b], v);
         }
       }
-      if (lane == 0 && my_vsum) atomicAdd(reinterpret_cast<unsigned long long*>(&st.total[s]), (unsigned long long)my_vsum);
     }
-#if defined(L5DH_EXP) && (L5DH_EXP & 64)
-    if (threadIdx.x == 0) s_item = item + gridDim.x;
-#else
     if (threadIdx.x == 0) s_item = gridDim.x + atomicAdd(ctr, 1u);
-#endif
     __syncthreads();  // the LDS rows are read: the next item may clear them; the next index visible
   }
 }
@@ -937,13 +834,13 @@ int num_cus() {
 
 hipError_t set_snapshot_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)acc_cold_p_lds(32));
+                                     (int)ACC_COLD_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
+  e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FOLD16_LDS);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_HOT_LDS);
+  return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FOLD32_LDS);
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
@@ -963,13 +860,13 @@ hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out
 }
 
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
-                             int final_mode, int reset, int stores_first, hipStream_t st) {
+                             int final_mode, int reset, hipStream_t st) {
   if (cold_items == 0) return hipSuccess;
   // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
   // may be DEV_COUNT (read on the device)
   const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
-  hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), acc_cold_p_lds(32), st, segs, plan, state, tb, out,
-                     cold_items, final_mode, reset, stores_first);
+  hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
+                     cold_items, final_mode, reset);
   return hipGetLastError();
 }
 
@@ -981,10 +878,10 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
   const size_t items = (n + chunk - 1) / chunk;
   const dim3 grid((uint32_t)std::min<size_t>(items, (size_t)num_cus()));
   if (state.S <= 16 && !wide)
-    hipLaunchKernelGGL(k_fold1<true>, grid, dim3(WG), ACC_SPLIT_LDS, st, series, values, n, chunk, state, tb, err,
+    hipLaunchKernelGGL(k_fold1<true>, grid, dim3(WG), FOLD16_LDS, st, series, values, n, chunk, state, tb, err,
                        vec ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_fold1<false>, grid, dim3(WG), ACC_HOT_LDS, st, series, values, n, chunk, state, tb, err,
+    hipLaunchKernelGGL(k_fold1<false>, grid, dim3(WG), FOLD32_LDS, st, series, values, n, chunk, state, tb, err,
                        vec ? 1 : 0);
   return hipGetLastError();
 }

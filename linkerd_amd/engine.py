@@ -243,6 +243,44 @@ class HistogramEngine:
         for i, e in enumerate(engines):
             e.nranks, e.rank = len(engines), i
 
+    @staticmethod
+    def comm_init_loopback(engines: Sequence["HistogramEngine"]) -> None:
+        """l5dh_comm_init_loopback: the engines (one device) as an n-rank group whose
+        collectives are device copies -- the multi-rank merge path on one GPU (tests)."""
+        arr = (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
+        rc = N.load().l5dh_comm_init_loopback(arr, len(engines))
+        if rc != 0:
+            engines[0]._check(rc, "l5dh_comm_init_loopback")
+        for i, e in enumerate(engines):
+            e.nranks, e.rank = len(engines), i
+
+    @staticmethod
+    def merge_all(engines: Sequence["HistogramEngine"], mode: int = N.MERGE_REDUCE_SCATTER, with_counts: bool = False):
+        """l5dh_merge_all over an l5dh_comm_init_all / loopback group: per rank
+        (first, count, summaries[, counts, totals]) as numpy."""
+        n = len(engines)
+        rows = engines[0].merge_rows(mode)
+        outs = [np.zeros(rows, dtype=N.SUMMARY_DTYPE) for _ in engines]
+        cnts = [np.zeros((rows, N.NBUCKETS), np.int32) for _ in engines] if with_counts else None
+        tots = [np.zeros(rows, np.int64) for _ in engines] if with_counts else None
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p).value  # noqa: E731
+        ctxs = (ctypes.c_void_p * n)(*[e._ctx.value for e in engines])
+        o_arr = (ctypes.c_void_p * n)(*[ptr(o) for o in outs])
+        c_arr = (ctypes.c_void_p * n)(*[ptr(c) for c in cnts]) if with_counts else None
+        t_arr = (ctypes.c_void_p * n)(*[ptr(t) for t in tots]) if with_counts else None
+        firsts, counts = (ctypes.c_uint32 * n)(), (ctypes.c_uint32 * n)()
+        rc = N.load().l5dh_merge_all(ctxs, n, int(mode), o_arr, c_arr, t_arr, firsts, counts)
+        if rc != 0:
+            engines[0]._check(rc, "l5dh_merge_all")
+        res = []
+        for i in range(n):
+            f, c = firsts[i], counts[i]
+            item = (f, c, outs[i][:c])
+            if with_counts:
+                item += (cnts[i][:c], tots[i][:c])
+            res.append(item)
+        return res
+
     def comm_destroy(self) -> None:
         self._check(self._lib.l5dh_comm_destroy(self._ctx), "l5dh_comm_destroy")
         self.nranks, self.rank = 1, 0

@@ -74,18 +74,26 @@ class CostModel:
         return self.fixed + self.per_sample * samples + self.per_series * series
 
 
-def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard]:
-    """Contiguous series ranges of equal modelled device time, from the previous
-    interval's records per 32-series tile (l5dh_tile_totals of the rank that held
-    them, or an expected load): a tile's records are spread evenly over its series
-    for the boundaries.  When the first tile alone, folded at ingest, costs less than
-    the slowest rank of the plain split, rank 0 takes exactly that tile and the other
-    ranks split the rest (a Zipf head concentrates there)."""
+def _per_series(tile_samples, S: int) -> np.ndarray:
+    """A per-tile load spread evenly over each tile's series (the last tile holds
+    S - 32 (F - 1) of them)."""
     t = np.asarray(tile_samples, dtype=np.float64)
     F = (S + 31) // 32
     if t.size != F:
         raise ValueError(f"tile_samples must hold {F} tiles")
-    per_series = np.repeat(t / 32.0, 32)[:S]
+    n = np.full(F, 32, dtype=np.int64)
+    n[-1] = S - 32 * (F - 1)
+    return np.repeat(t / n, n)
+
+
+def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard]:
+    """Contiguous series ranges of equal modelled device time, from a per-tile load:
+    the records per 32-series tile of the last binned batch (l5dh_tile_totals of the
+    rank that held them -- the previous interval's last batch -- or an expected
+    load); a tile's records are spread evenly over its series for the boundaries.  When the first tile alone, folded at ingest, costs less than
+    the slowest rank of the plain split, rank 0 takes exactly that tile and the other
+    ranks split the rest (a Zipf head concentrates there)."""
+    per_series = _per_series(tile_samples, S)
     w = cost.per_sample * per_series + cost.per_series
     plain = shard_ranges(S, world, weights=w)
     if world == 1 or S <= 32:
@@ -103,8 +111,7 @@ def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard
 
 def plan_ms(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) -> List[float]:
     """Modelled device time (ms) of every rank of a plan."""
-    t = np.asarray(tile_samples, dtype=np.float64)
-    per_series = np.repeat(t / 32.0, 32)[:S]
+    per_series = _per_series(tile_samples, S)
     return [cost.range_ms(float(per_series[x.first:x.first + x.count].sum()), x.count) if x.count else 0.0
             for x in shards]
 
@@ -114,12 +121,16 @@ def plan_spread(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) 
     one-tile rank 0 (plan_shards) cannot take more work without losing its fold, so
     it only has to stay at or below the others' maximum; the spread is of the rest."""
     ms = plan_ms(shards, tile_samples, S, cost)
+
+    def ratio(hi: float, lo: float) -> float:
+        return hi / lo if lo > 0 else float("inf")  # (a rank with no modelled time: unbalanced)
+
     if len(shards) > 1 and shards[0].count <= 32 < S:
         if ms[0] > max(ms[1:]):
-            return ms[0] / min(ms[1:])
+            return ratio(ms[0], min(ms[1:]))
         ms = ms[1:]
     ms = [m for m in ms if m > 0]
-    return max(ms) / min(ms)
+    return ratio(max(ms), min(ms)) if ms else 1.0
 
 
 class SeriesRouter:

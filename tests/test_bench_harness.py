@@ -69,3 +69,26 @@ def test_c4_ranks_split_the_samples():
     assert all(p["count"] == 1_000_000 and p["first"] == 0 for p in plans)
     assert sum(p["samples"] for p in plans) == 1_000_000_000
     assert plans[1]["base_index"] == plans[0]["samples"]
+
+
+def test_plan_keeps_the_last_partial_tiles_load():
+    """with S % 32 != 0 the last tile's load is spread over its real series
+    count (none of it dropped), and a zero-time rank gives an infinite spread rather
+    than a ZeroDivisionError."""
+    import numpy as np
+    from linkerd_amd import fleet
+    S = 32 * 10 + 7
+    t = np.arange(1, 12, dtype=np.float64) * 1000.0
+    cost = fleet.CostModel(per_sample=1e-6, per_series=1e-4, per_sample_fold=1e-6, fixed=0.0)
+    per = fleet._per_series(t, S)
+    assert per.size == S and abs(per.sum() - t.sum()) < 1e-6
+    assert np.allclose(per[-7:], t[-1] / 7)
+    shards = fleet.plan_shards(t, S, 3, cost)
+    assert sum(x.count for x in shards) == S
+    ms = fleet.plan_ms(shards, t, S, cost)
+    assert abs(sum(ms) - sum(cost.range_ms(float(per[x.first:x.first + x.count].sum()), x.count)
+                            for x in shards)) < 1e-9
+    zero = fleet.CostModel(per_sample=0.0, per_series=0.0, per_sample_fold=0.0, fixed=0.0)
+    assert fleet.plan_spread(shards, t, S, zero) == 1.0
+    lopsided = [fleet.Shard(0, 0, 32), fleet.Shard(1, 32, S - 32), fleet.Shard(2, S, 0)]
+    assert fleet.plan_spread(lopsided, t, S, cost) >= 1.0

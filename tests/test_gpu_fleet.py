@@ -79,3 +79,77 @@ def test_export_reset_fused_matches_oracle(oracle, dev_bufs):
     np.testing.assert_array_equal(counts, o2.counts())
     np.testing.assert_array_equal(totals, o2.totals())
     eng.close()
+
+
+def _oracle_of(oracle, S, parts):
+    o = oracle.OracleHistograms(S)
+    for s, v in parts:
+        o.ingest(s, v)
+    return o
+
+
+@pytest.mark.parametrize("mode", [N.MERGE_REDUCE_SCATTER, N.MERGE_ALL_REDUCE], ids=["reduce_scatter", "all_reduce"])
+@pytest.mark.parametrize("W", [2, 3, 8])
+def test_loopback_multirank_merge(oracle, W, mode):
+    """The W > 1 merge code on one GPU (l5dh_comm_init_loopback): per-destination
+    slices of the sparse encoding, the size all-gather, the payload exchange, the
+    local slice decoded in place, the totals' reduce-scatter -- or the dense
+    all-reduce -- with S not divisible by W, an escaped count (> 2^21 - 1 samples of
+    one bucket on one rank) and two merge intervals through the same buffers."""
+    from linkerd_amd.engine import HistogramEngine
+    S = 4001
+    engines = [HistogramEngine(S) for _ in range(W)]
+    try:
+        HistogramEngine.comm_init_loopback(engines)
+        with pytest.raises(N.L5dhError):
+            engines[0].merge(mode)  # a loopback group merges through l5dh_merge_all only
+        for interval in range(2):
+            series, vals = synth.c3(S=S, N=300_000 + 50_000 * interval, seed=60 + 7 * W + interval)
+            parts = []
+            for r, e in enumerate(engines):
+                p = (series[r::W], vals[r::W])
+                e.ingest(*p)
+                parts.append(p)
+            if interval == 0:  # series 17: one bucket past the encoding's count field, on the last rank
+                heavy = (np.full(2_100_000, 17, np.uint32), np.full(2_100_000, 3.0, np.float32))
+                engines[-1].ingest(*heavy)
+                parts.append(heavy)
+            o = _oracle_of(oracle, S, parts)
+            want_c, want_t, want_s = o.counts(), o.totals(), o.snapshot()
+            res = HistogramEngine.merge_all(engines, mode, with_counts=True)
+            per = -(-S // W)
+            for r, (first, count, summ, cnt, tot) in enumerate(res):
+                if mode == N.MERGE_REDUCE_SCATTER:
+                    assert (first, count) == (min(r * per, S), max(0, min(per, S - r * per)))
+                else:
+                    assert (first, count) == (0, S)
+                sl = slice(first, first + count)
+                np.testing.assert_array_equal(cnt, want_c[sl])
+                np.testing.assert_array_equal(tot, want_t[sl])
+                assert summ.tobytes() == want_s[sl].tobytes()
+            if mode == N.MERGE_REDUCE_SCATTER:
+                assert all(e.merge_bytes()["sent"] > 0 for e in engines)
+            for e in engines:  # the export consumed every rank's interval
+                after = e.snapshot(reset=False)
+                assert not after["count"].any() and not after["sum"].any()
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_comm_rejects_more_than_64_ranks_before_any_state_is_consumed(oracle):
+    """the sparse reduce-scatter holds <= 64 sources; a larger communicator
+    is refused at init (not inside a merge, after the export consumed the interval)."""
+    from linkerd_amd.engine import HistogramEngine
+    S = 300
+    series, vals = synth.c3(S=S, N=50_000, seed=71)
+    eng = HistogramEngine(S)
+    try:
+        eng.ingest(series, vals)
+        with pytest.raises(N.L5dhError):
+            eng.comm_init_rank(HistogramEngine.comm_unique_id(), 65, 0)
+        got = eng.snapshot(reset=True)
+        o = _oracle_of(oracle, S, [(series, vals)])
+        assert got.tobytes() == o.snapshot().tobytes()
+    finally:
+        eng.close()

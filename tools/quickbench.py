@@ -1,4 +1,5 @@
-"""Quick perf probe: C2 (100k series x 1k samples) ingest + snapshot, per-kernel times."""
+"""Quick perf probe: C2 (100k series x 1k samples) ingest + snapshot, per-kernel times.
+  python tools/quickbench.py [S] [K] [region_pct] [zipf]"""
 import sys, time, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -8,7 +9,7 @@ from linkerd_amd.engine import HistogramEngine
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000
-MODE = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+PCT = int(sys.argv[3]) if len(sys.argv) > 3 else 100  # L5DH_PARAM_REGION_PCT (< 100: the redo path)
 t0 = time.time()
 if len(sys.argv) > 4 and sys.argv[4] == "zipf":
     series, vals = synth.c3(S=S, N=S * K)
@@ -21,8 +22,8 @@ eng = HistogramEngine(S)
 summ = torch.zeros(S * 11, dtype=torch.int64, device="cuda")
 cnt = torch.zeros((S, 1798), dtype=torch.int32, device="cuda")
 eng.set_param(N.PARAM_TIMING, 1)
-eng.set_param(N.PARAM_BIN_MODE, MODE)
-print("mode", MODE)
+eng.set_param(N.PARAM_REGION_PCT, PCT)
+print("region pct", PCT)
 for it in range(5):
     torch.cuda.synchronize()
     t = time.perf_counter()
