@@ -481,7 +481,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   // level 2's exact layout in any case (N + 7 per key of padding)
   const size_t cap32 = n + n / 2 + ((size_t)1 << 19);
   const size_t cap16 = 2 * n + n / 8 + (size_t)128 * c->F + 4096;
-  const size_t dlim16 = cap16 - (n + (size_t)16 * c->F + 1024);
+  const size_t dlim16 = (cap16 - (n + (size_t)16 * c->F + 1024)) & ~(size_t)7;  // (level-2 regions 16-B aligned)
   {
     int r = ensure(c, sg.rec32, (cap32 + 16) * 4);  // readers load whole 16-B groups
     if (!r) r = ensure(c, sg.rec16, (cap16 + 16) * 2);

@@ -1,8 +1,8 @@
 // l5dh_ingest.hip -- ingest-side kernels (Metric.Stat.add, batched): a two-level
 // partition of the COO batch into capacity-planned regions, with no counting pass.
 //
-//   k_rsample  ids of 2^20 evenly spaced samples (every sample of a smaller batch)
-//              counted per (tile, half) key
+//   k_rsample  2^20 sampled ids (runs of 64 at 2^14 evenly spaced places; every
+//              sample of a smaller batch) counted per (tile, half) key
 //   k_rplan1   this batch's direct tiles (the biggest estimated) and the level-1 bin
 //              regions (super-tiles; two half-bins per direct tile), sized from the
 //              previous batch's exact key counts and this batch's sample
@@ -99,7 +99,9 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
   const uint64_t per = (m + RS_WG - 1) / RS_WG;
   const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
   for (uint64_t k = k0 + threadIdx.x; k < k1; k += 1024) {
-    const uint64_t i = m == n ? k : k * n / m;  // evenly spaced draws
+    // runs of 64 consecutive ids at 2^14 evenly spaced places (one coalesced 256-B read
+    // per wave, not one line per draw); every id when the batch is <= 2^20
+    const uint64_t i = m == n ? k : (k >> 6) * n / (m >> 6) + (k & 63u);
     const uint32_t s = series[i];
     if (s < S) {
       const uint32_t key = s >> 4;
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // written out in order: each entry's run is the number of run heads at or before
 // it -- a per-64-entry group prefix (gpre) plus a popcount of the group's bits of
 // the run-head bitmap -- indexing the runs' destination deltas (rdelta[run] = run
-// base - stage offset, or INVALID).  Runs below the first direct bin's rank are u32
+// base - stage offset, or NODEST).  Runs below the first direct bin's rank are u32
 // records (rec32), the others u16 (rec16).  A run that does not fit is dropped and
 // flagged; pass 1 (the redo) exits unless k_rfix1 asked for it and adds nothing to
 // sumfix or the error counter.
@@ -315,6 +317,9 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
 // lut2 [1024] uint2, direct sums [255 x 32].
 constexpr int CHW = 24576;
+// rdelta of a dropped run: a valid delta (run base - stage offset) lies in (-CHW, cap16),
+// cap16 < 2^32 - CHW - 1, so -(CHW + 1) never is one (0xFFFFFFFF is: base 0 at offset 1)
+constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 #ifndef L5DH_RBIN1_NT
 #define L5DH_RBIN1_NT 768
 #endif
@@ -442,18 +447,28 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           const uint32_t di = dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw));
           const uint32_t p = pl[q];
           uint32_t o;
+#if defined(L5DH_EXP) && (L5DH_EXP & 4)  // timing only: no bucket search
+          const uint32_t bk = p & 2047u;
+          (void)lv;
+#else
           const uint32_t bk = lut2_decode(p, lv[q], o);
+#endif
           const bool esc = p >= V_ESC;
           const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
           rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
+#if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only: no value sums
+#elif defined(L5DH_EXP) && (L5DH_EXP & 2)  // timing only: value sums without the wrap check
+          if (direct && !esc && p != 0u && pass == 0) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
+#else
           if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
             const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
             if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
               atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
           }
+#endif
         }
         // slots 4 (kk NT + thread) + q of this group kk, as loaded
         *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4) * NT + threadIdx.x)) =
@@ -551,7 +566,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     for (int j = 0; j < RB; ++j) {
       const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
       if (rn[j]) {
-        uint32_t d = INVALID;
+        uint32_t d = NODEST;
         if (rb_bin < TB) {
           if (rold[j] + rn[j] <= rcapv[j]) d = rbase[j] + rold[j] - (offr[rb_bin] & 0xFFFFu);
           else hdr[H_OV1] = 1u;  // this run is dropped; k_rfix1 has the batch redone with exact regions
@@ -571,7 +586,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
-      if (d != INVALID) {
+      if (d != NODEST) {
         if (run < nst)
           rec32[i + d] = stage[i];
         else

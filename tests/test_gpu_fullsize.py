@@ -64,10 +64,11 @@ def test_c3_full_size_invariants_and_sampled_oracle(oracle):
     order = summ[live][:, [1, 4, 5, 6, 7, 8, 9, 2]]  # min p50 p90 p95 p99 p999 p9999 max
     assert bool((order[:, 1:] >= order[:, :-1]).all()), "percentiles out of order"
 
-    # bit-exact oracle replay of sampled series: direct/split tiles (ids < 8192 are
-    # the hottest tiles of this Zipf head) and cold tiles
+    # bit-exact oracle replay of sampled series: the Zipf head (series 0 alone holds
+    # 6.95 % of the batch, 0-2 together 12.7 %), direct/split tiles (ids < 8192 are
+    # the hottest tiles) and cold tiles
     rng = np.random.default_rng(5)
-    chosen = np.unique(np.concatenate([[3, 9, 17, 33, 100, 517, 1024, 1500, 4095, 8191],
+    chosen = np.unique(np.concatenate([[0, 1, 2, 3, 9, 17, 33, 100, 517, 1024, 1500, 4095, 8191],
                                        rng.integers(8192, S, size=54)])).astype(np.int64)
     sel = torch.from_numpy(chosen).to(dev)
     m = torch.isin(series, sel.to(torch.int32))
@@ -85,3 +86,64 @@ def test_c3_full_size_invariants_and_sampled_oracle(oracle):
     eng.close()
     del series, values, rows, summ, m
     torch.cuda.empty_cache()
+
+
+def _gen_c3(lib, series, values, S, seed, stream):
+    import torch
+    cdf = torch.from_numpy(synth.zipf_cdf(S)).to(series.device)
+    rc = lib.l5ds_gen_zipf(ctypes.c_void_p(series.data_ptr()), ctypes.c_void_p(values.data_ptr()),
+                           ctypes.c_uint64(series.numel()), ctypes.c_uint64(S), ctypes.c_void_p(cdf.data_ptr()),
+                           ctypes.c_uint64(seed), ctypes.c_double(0.8), ctypes.c_uint64(0), ctypes.c_uint32(0),
+                           ctypes.c_void_p(stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+
+
+def test_c3_whole_batches_bucket_exact(oracle):
+    """Every bucket of whole C3 batches (1e9 samples each) against a torch ground truth:
+    bincount of series * 1798 + upper_bound(limits, (long)value) -- the
+    Arrays.binarySearch insertion rule of BucketedHistogram.add (Metric.scala:30-33),
+    computed with torch.searchsorted, independent of the engine's LUTs and kernels --
+    plus the exact per-series sums and counts of the summaries.  Three batches in a
+    row through one engine (seeds 3, 4, 3: the bench's rotation), so the second and
+    third are binned with regions planned from a different previous batch."""
+    import torch
+    from linkerd_amd.engine import HistogramEngine
+    S, n = 1_000_000, 1_000_000_000
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    lib = ctypes.CDLL(N.SYNTH_PATH)
+    lib.l5ds_gen_zipf.restype = ctypes.c_int
+    series = torch.empty(n, dtype=torch.int32, device=dev)
+    values = torch.empty(n, dtype=torch.float32, device=dev)
+    lim = torch.from_numpy(oracle.limits().astype(np.int64)).to(dev)  # the oracle's makeLimitsFor
+    eng = HistogramEngine(S)
+    rows = torch.empty((S, N.NBUCKETS), dtype=torch.int32, device=dev)
+    summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
+    try:
+        for seed in (3, 4, 3):
+            _gen_c3(lib, series, values, S, seed, stream)
+            eng.ingest(series, values)
+            eng.snapshot_into(summ, rows, reset=True)
+            torch.cuda.synchronize()
+            truth = torch.zeros(S * N.NBUCKETS, dtype=torch.int32, device=dev)
+            sums = torch.zeros(S, dtype=torch.int64, device=dev)
+            step = 100_000_000
+            for o in range(0, n, step):
+                ids = series[o:o + step].long()
+                v = values[o:o + step].to(torch.int64)  # values in [0, 1e9]: (long)value
+                b = torch.searchsorted(lim, v, right=True)
+                truth.index_add_(0, ids * N.NBUCKETS + b, torch.ones_like(b, dtype=torch.int32))
+                sums.index_add_(0, ids, v)
+                del ids, v, b
+            truth = truth.view(S, N.NBUCKETS)
+            bad = (rows != truth).any(dim=1)
+            assert int(bad.sum()) == 0, f"seed {seed}: {int(bad.sum())} series differ, first {torch.nonzero(bad)[:8].flatten().tolist()}"
+            assert torch.equal(summ[:, 0], truth.sum(dim=1, dtype=torch.int64)), f"seed {seed}: counts"
+            assert torch.equal(summ[:, 3], sums), f"seed {seed}: sums"
+            del truth, sums, bad
+    finally:
+        eng.close()
+        del series, values, rows, summ
+        torch.cuda.empty_cache()

@@ -508,3 +508,26 @@ def test_tile_totals_are_the_batch_load(regime):
             np.testing.assert_array_equal(e.tile_totals(), want)
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("n", [60_000, 150_000])
+def test_direct_run_delta_at_region_start(oracle, n):
+    """A direct half-bin whose region starts at rec16 index 0 while its run sits at
+    stage offset 1 (one super-tile record before it) has the run delta 0 - 1 =
+    0xFFFFFFFF: it must not read as a dropped run.  All tiles but the last are direct
+    (S = 4001: tile 125 holds one series), one slab."""
+    from linkerd_amd.engine import HistogramEngine
+    S = 4001
+    series, vals = synth.c3(S=S, N=2 * n, seed=74)
+    s, v = series[0::2], vals[0::2]
+    eng = HistogramEngine(S)
+    try:
+        eng.set_param(N.PARAM_MAX_SLABS, 1)
+        eng.ingest(s, v)
+        counts, totals = eng.export_state(reset=True)
+        o = oracle.OracleHistograms(S)
+        o.ingest(s, v)
+        np.testing.assert_array_equal(counts, o.counts())
+        np.testing.assert_array_equal(totals, o.totals())
+    finally:
+        eng.close()
