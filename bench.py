@@ -17,7 +17,11 @@ Workloads (synthetic inputs generated on the GPU):
                 collective, strong scaling.
   c4            fleet merge: the same 1M series, the 1e9 samples sample-sharded
                 over the ranks; each rank ingests its share and calls l5dh_merge
-                (export + RCCL reduce-scatter + summaries of its slice).
+                (sparse export + RCCL exchange + dense rows and summaries of its
+                slice).  `--loopback W` (or `--shard r/W`) runs the whole W-rank merge on
+                this one GPU: W contexts, each ingesting its share, merged through
+                l5dh_merge_all over the loopback transport (device copies instead of
+                xGMI) -- every rank's work, so the per-rank time is ms_per_step / W.
   c2            100k series x 1k samples on one GPU (replicas when N > 1).
   c1            1 series x 1e7 samples (replicas when N > 1).
 --piece P streams the batch from pinned host memory in P-sample l5dh_ingest
@@ -87,6 +91,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=None, help="oracle threads (default: c1 1, else the host's)")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_latest.json"))
     p.add_argument("--dry-run", action="store_true", help="ranks + shard plan only (gloo, no GPU, no engine)")
+    p.add_argument("--loopback", type=int, default=0,
+                   help="c4: the whole W-rank fleet merge on this GPU (W contexts, loopback transport)")
     return p.parse_args()
 
 
@@ -299,8 +305,104 @@ def result_stream():
     return out
 
 
+def run_c4_loopback(args, result_out):
+    """C4 on one GPU: the W ranks of a sample-sharded fleet as W contexts of this
+    device, each ingesting its share of the 1e9 samples, merged by l5dh_merge_all over
+    the loopback transport (l5dh_comm_init_loopback: the same encode / size / payload /
+    decode steps as RCCL, the exchange by device copies).  A step is the whole fleet's
+    work: every rank's ingest, sparse export, exchange, and the dense rows + summaries
+    of every slice (device outputs).  Per-rank time = ms_per_step / W (the ranks' work
+    is serialized on this GPU); B_alg = 8 N + 7280 S for the fleet, once."""
+    import torch
+    from linkerd_amd import _native as N_
+    from linkerd_amd.engine import HistogramEngine
+    W = args.loopback
+    torch.cuda.set_device(0)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    synth_lib = ctypes.CDLL(N_.SYNTH_PATH)
+    synth_lib.l5ds_gen_zipf.restype = ctypes.c_int
+    plans = [plan(args, W, r) for r in range(W)]
+    S, Ntot = plans[0]["count"], plans[0]["N_total"]
+    batches = [gen_batch(torch, synth_lib, p, 0, stream) for p in plans]
+    engines = [HistogramEngine(S, device=0) for _ in range(W)]
+    for e in engines:
+        e.set_stream(stream)
+    HistogramEngine.comm_init_loopback(engines)
+    rows = engines[0].merge_rows(N_.MERGE_REDUCE_SCATTER)
+    summ = [torch.empty((rows, 11), dtype=torch.int64, device=dev) for _ in range(W)]
+    cnts = [torch.empty((rows, N_.NBUCKETS), dtype=torch.int32, device=dev) for _ in range(W)]
+    lib = N_.load()
+    ctxs = (ctypes.c_void_p * W)(*[e._ctx.value for e in engines])
+    o_arr = (ctypes.c_void_p * W)(*[t.data_ptr() for t in summ])
+    c_arr = (ctypes.c_void_p * W)(*[t.data_ptr() for t in cnts])
+    firsts, counts = (ctypes.c_uint32 * W)(), (ctypes.c_uint32 * W)()
+
+    def step():
+        for e, b in zip(engines, batches):
+            e.ingest(*b)
+        rc = lib.l5dh_merge_all(ctxs, W, N_.MERGE_REDUCE_SCATTER, o_arr, c_arr, None, firsts, counts)
+        if rc != 0:
+            engines[0]._check(rc, "l5dh_merge_all")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    got = sum(int(summ[r][:counts[r], 0].sum()) for r in range(W))
+    assert got == Ntot, f"summary counts sum {got} != {Ntot}"
+    assert sum(int(cnts[r][:counts[r]].sum(dtype=torch.int64)) for r in range(W)) == Ntot
+    for e in engines:
+        e.set_param(N_.PARAM_TIMING, 1)
+        e.kernel_times(reset=True)
+    tsteps = 3
+    for _ in range(tsteps):
+        step()
+    per_rank = []
+    for e in engines:
+        kt = e.kernel_times(reset=True)
+        per_rank.append({k: round(ms / tsteps, 4) for k, (ms, n) in kt.items() if n})
+        e.set_param(N_.PARAM_TIMING, 0)
+    mb = [e.merge_bytes() for e in engines]
+    ms = elapsed / args.steps * 1e3
+    balg = 8 * Ntot + 7280 * S
+    path_gbs = balg / (ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": Ntot * args.steps / elapsed, "unit": "samples/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C4: fleet merge, 1M series, 1e9 Zipf(s=1) samples per step sample-sharded over "
+                               f"{W} ranks, all {W} ranks on this one GPU (l5dh_comm_init_loopback)",
+                   "series_total": S, "samples_per_step": Ntot, "ranks": W,
+                   "step": "every rank: ingest + sparse export; exchange (device copies); every slice's dense rows "
+                           "+ summaries", "per_rank_ms": round(ms / W, 4)},
+        "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(path_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_step": balg,
+                          "formula": "8 B/sample + 7280 B/series for the fleet, once (SURVEY.md §8d)"},
+        "per_rank_kernels_ms": per_rank,
+        "merge": {"encoded_bytes": [m["encoded"] for m in mb], "sent_bytes": [m["sent"] for m in mb],
+                  "dense_bytes_per_rank": mb[0]["dense"] * (W - 1) // W,
+                  "note": "sent = what a rank sends the other W-1 ranks (sparse); dense = the dense rows + totals "
+                          "a dense reduce-scatter would send"},
+        "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(line), file=result_out, flush=True)
+    for e in engines:
+        e.close()
+
+
 def run(args):
     result_out = result_stream()
+    if args.workload == "c4" and (args.loopback or args.shard):
+        if args.shard and not args.loopback:
+            args.loopback = int(args.shard.split("/")[1])
+        args.shard = None
+        return run_c4_loopback(args, result_out)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

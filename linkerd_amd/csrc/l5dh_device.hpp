@@ -215,6 +215,56 @@ __device__ __forceinline__ uint32_t merge_words4(uint4 v) {
          (v.z >= MERGE_CMAX) + (v.w >= MERGE_CMAX);
 }
 
+// A dirty row's counts: the new records' (LDS) plus the state row's.
+template <class A, class B>
+struct SrcSum2 {
+  A a;
+  B b;
+  __device__ __forceinline__ uint4 get4(int b0) const {
+    const uint4 x = a.get4(b0), y = b.get4(b0);
+    return make_uint4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+};
+
+// The fleet merge's encoding of one row (one wave): its words, then its entries at
+// enc[at..) in bucket order -- bucket << 21 | count, or bucket << 21 | MERGE_CMAX
+// followed by the count (l5dh_merge.hip decodes them).  Lane l covers bins 4q..4q+3,
+// q = l + 64 k.
+template <class Src>
+__device__ __forceinline__ uint32_t row_words(const Src& src) {
+  const int lane = lane_id();
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int q = lane + 64 * k;
+    if (q < NB4) w += merge_words4(src.get4(4 * q));
+  }
+  return (uint32_t)wave_sum((uint64_t)w);
+}
+template <class Src>
+__device__ __forceinline__ void row_encode(const Src& src, uint32_t* __restrict__ enc, uint32_t at) {
+  const int lane = lane_id();
+#pragma unroll 2
+  for (int k = 0; k < 8; ++k) {
+    const int q = lane + 64 * k;
+    const uint4 v = q < NB4 ? src.get4(4 * q) : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t w = merge_words4(v);
+    const uint32_t incl = wave_incl_scan32(w);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t pos = at + incl - w;
+    const uint32_t c[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (c[j]) {
+        const bool esc = c[j] >= MERGE_CMAX;
+        enc[pos++] = ((uint32_t)(4 * q + j) << 21) | (esc ? MERGE_CMAX : c[j]);
+        if (esc) enc[pos++] = c[j];
+      }
+    }
+    at += total;
+  }
+}
+
 // A wave's per-lane word counts -> *out (lane 0), when out is non-null.
 __device__ __forceinline__ void put_words(uint32_t w, uint32_t* __restrict__ out) {
   if (out == nullptr) return;

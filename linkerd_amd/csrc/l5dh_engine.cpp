@@ -181,6 +181,7 @@ struct l5dh_ctx {
   uint32_t* d_hot_list = nullptr;
   uint8_t* d_tile_flags = nullptr;
   uint32_t* d_header = nullptr;
+  uint32_t* d_enc_base = nullptr;  // [F] sparse export: each tile's first word of the unpacked encoding
   uint32_t* h_header = nullptr;      // pinned: [4] ingest error count (written by k_rfix1)
   uint32_t* h_header_dev = nullptr;  // its device-side address
   uint32_t* d_kest = nullptr;   // [2F] sampled ids per (tile, half) key of the batch being binned
@@ -218,6 +219,8 @@ struct l5dh_ctx {
   DevBuf merge_counts, merge_totals, recv_counts, recv_totals;
   // sparse reduce-scatter (l5dh_merge.hip): this rank's encoding, the received slices
   DevBuf m_words, m_offs, m_enc, m_tmp, m_sizes, r_words, r_offs, r_enc;
+  DevBuf m_unpacked, m_roff;  // the sparse export: rows' encodings at their tiles' places, each row's first word
+  bool m_sparse = false;      // the last export was sparse (reduce-scatter through the collective)
   size_t m_tmp_bytes = 0;
   std::vector<uint64_t> m_to, m_from;  // words to / from every rank
   uint64_t m_dense_bytes = 0, m_encoded_bytes = 0, m_sent_bytes = 0;
@@ -353,8 +356,8 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot, c->d_cold_item, static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags,
-              c->d_header};
+  return Plan{c->d_tile_tot, c->d_enc_base, c->d_cold_item, static_cast<uint2*>(c->split_item.p), c->d_hot_list,
+              c->d_tile_flags, c->d_header};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -368,8 +371,9 @@ Segs segs_view(l5dh_ctx* c) {
 }
 
 // Aggregate every pending segment.  final_mode: emit summaries/counts for the
-// whole series space into `out` (fused path); otherwise fold into state.
-int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
+// whole series space into `out` (fused path); otherwise fold into state.  encode: the
+// fleet merge's sparse export (out.words / out.roff / out.totals; out.enc is set here).
+int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode = false) {
   if (!final_mode && c->nseg == 0) return 0;
   Segs sv = segs_view(c);
   size_t recs = 0;
@@ -387,9 +391,21 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out) {
   // straight into their output rows (no copy of state rows in k_hot_finish), and those
   // whose halves are one item each are written by their items alone (TF_SOLO)
   const int direct_out = final_mode && reset && out.counts && out.first == 0 && out.count == (uint32_t)c->S;
+  // the sparse export (the fleet merge's reduce-scatter): row encodings, no dense rows
+  if (encode && !(final_mode && reset && out.first == 0 && out.count == (uint32_t)c->S && !out.counts && !out.summ))
+    return fail(c, -EINVAL, "internal: the sparse export is a whole-range resetting export");
   {
     KTimer kt(c, L5DH_K_SCAN);
-    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, hc, c->d_dirty, direct_out, pl, c->stream));
+    HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, hc, c->d_dirty, direct_out, encode ? 1 : 0, pl,
+                          c->stream));
+  }
+  if (encode) {  // the unpacked encoding's size comes from the plan (one host wait)
+    uint32_t words = 0;
+    HIPCHK(c, hipMemcpyAsync(&words, c->d_header + 5 + 4 * ((c->F + 1023) / 1024), 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int r = ensure(c, c->m_unpacked, (size_t)words * 4 + 16)) return r;
+    out.enc = static_cast<uint32_t*>(c->m_unpacked.p);
   }
   // The accumulate kernels are persistent and read their item counts from the plan
   // header on the device, so no host round trip separates them from the plan: the
@@ -684,25 +700,32 @@ uint32_t merge_per(const l5dh_ctx* c) { return (c->S + c->nranks - 1) / c->nrank
 
 // Phase 1: pending samples + state -> dense rows [Sp][1798] and totals [Sp] (the
 // fused whole-range export with reset), pad rows zero.
-int merge_export(l5dh_ctx* c) {
+bool merge_skips_collective(const l5dh_ctx* c);
+
+int merge_export(l5dh_ctx* c, int mode) {
   if (!c->comm && !c->loopback)
     return fail(c, -EINVAL, "no communicator: call l5dh_comm_init_rank or l5dh_comm_init_all first");
   int r = flush_ring(c);
   if (r) return r;
   const size_t Sp = (size_t)merge_per(c) * c->nranks;
-  if ((r = ensure(c, c->merge_counts, Sp * NB * 4)) || (r = ensure(c, c->merge_totals, Sp * 8))) return r;
-  // the encoding's words per row come out of the export itself (every kernel that
-  // emits a row counts its non-empty buckets), so the rows are read once, by k_menc
-  if ((r = ensure(c, c->m_words, (Sp + 1) * 4))) return r;
-  int32_t* cnt = static_cast<int32_t*>(c->merge_counts.p);
+  // the reduce-scatter through the collective exports SPARSE: each row's encoding straight
+  // from the accumulate kernels' bins (no dense rows, no re-read), words and first word per
+  // row; the all-reduce and a 1-rank communicator that skips the collective export dense rows
+  c->m_sparse = mode == L5DH_MERGE_REDUCE_SCATTER && !merge_skips_collective(c);
+  if ((r = ensure(c, c->merge_totals, Sp * 8)) || (r = ensure(c, c->m_words, (Sp + 1) * 4))) return r;
   int64_t* tot = static_cast<int64_t*>(c->merge_totals.p);
   uint32_t* words = static_cast<uint32_t*>(c->m_words.p);
-  if (Sp > c->S) {
-    HIPCHK(c, hipMemsetAsync(cnt + (size_t)c->S * NB, 0, (Sp - c->S) * NB * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(tot + c->S, 0, (Sp - c->S) * 8, c->stream));
-  }
+  if (Sp > c->S) HIPCHK(c, hipMemsetAsync(tot + c->S, 0, (Sp - c->S) * 8, c->stream));
   HIPCHK(c, hipMemsetAsync(words + c->S, 0, (Sp + 1 - c->S) * 4, c->stream));
-  return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot, words});
+  if (c->m_sparse) {
+    if ((r = ensure(c, c->m_roff, Sp * 4))) return r;
+    Outputs o{nullptr, nullptr, 0, c->S, tot, words, nullptr, static_cast<uint32_t*>(c->m_roff.p)};
+    return aggregate(c, 1, 1, o, true);
+  }
+  if ((r = ensure(c, c->merge_counts, Sp * NB * 4))) return r;
+  int32_t* cnt = static_cast<int32_t*>(c->merge_counts.p);
+  if (Sp > c->S) HIPCHK(c, hipMemsetAsync(cnt + (size_t)c->S * NB, 0, (Sp - c->S) * NB * 4, c->stream));
+  return aggregate(c, 1, 1, Outputs{nullptr, cnt, 0, c->S, tot, words, nullptr, nullptr});
 }
 
 // Phase 2 (reduce-scatter): the rows are exchanged sparse (l5dh_merge.hip) -- per
@@ -734,8 +757,12 @@ int merge_encode_step(l5dh_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(&bnd[q], offs + (size_t)q * per, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((r = ensure(c, c->m_enc, (size_t)bnd[W] * 4 + 16))) return r;
-  HIPCHK(c, merge_encode(static_cast<const int32_t*>(c->merge_counts.p), Sp, offs, static_cast<uint32_t*>(c->m_enc.p),
-                         c->stream));
+  if (c->m_sparse)  // the export's row encodings packed in row order (one contiguous slice per destination)
+    HIPCHK(c, merge_pack(static_cast<const uint32_t*>(c->m_unpacked.p), static_cast<const uint32_t*>(c->m_roff.p),
+                         words, offs, Sp, static_cast<uint32_t*>(c->m_enc.p), c->stream));
+  else
+    HIPCHK(c, merge_encode(static_cast<const int32_t*>(c->merge_counts.p), Sp, offs,
+                           static_cast<uint32_t*>(c->m_enc.p), c->stream));
   c->m_to.assign(W, 0);
   for (int q = 0; q < W; ++q) c->m_to[q] = bnd[q + 1] - bnd[q];
   c->m_dense_bytes = (uint64_t)Sp * (NB * 4 + 8);
@@ -1070,7 +1097,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_tile_tot, F * 4) &&
             mal((void**)&c->d_cold_item, (F + 1) * 16) && mal((void**)&c->d_hot_list, F * 4) &&
-            mal((void**)&c->d_header, (4 + 4 * ((F + 1023) / 1024)) * 4) && mal((void**)&c->d_tile_flags, F) &&
+            mal((void**)&c->d_header, plan_header_words((uint32_t)F) * 4) && mal((void**)&c->d_tile_flags, F) &&
+            mal((void**)&c->d_enc_base, F * 4) &&
             mal((void**)&c->d_kest, 2 * F * 4) && mal((void**)&c->d_kprev, 2 * F * 4);
   const size_t meta_bytes = (size_t)meta_layout((uint32_t)F).words() * 4;
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].meta, meta_bytes);
@@ -1117,7 +1145,7 @@ int l5dh_close(l5dh_ctx* c) {
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid,      c->d_base,     c->d_lut,       c->d_lut2,     c->d_counts,
                   c->d_total,   c->d_sumfix,   c->d_dirty,    c->d_err,       c->d_tile_tot, c->d_cold_item,
-                  c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev};
+                  c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev, c->d_enc_base};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {
@@ -1131,7 +1159,7 @@ int l5dh_close(l5dh_ctx* c) {
                     &c->ring_series,     &c->ring_values,  &c->merge_counts,   &c->merge_totals,
                     &c->recv_counts,     &c->recv_totals,  &c->m_words,        &c->m_offs,
                     &c->m_enc,           &c->m_tmp,        &c->m_sizes,        &c->r_words,
-                    &c->r_offs,          &c->r_enc};
+                    &c->r_offs,          &c->r_enc,        &c->m_unpacked,     &c->m_roff};
   for (DevBuf* b : bufs)
     if (b->p) hipFree(b->p);
   if (c->h_header) hipHostFree(c->h_header);
@@ -1517,7 +1545,7 @@ int l5dh_merge(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, in
   hipSetDevice(c->device);
   if (c->loopback) return fail(c, -EINVAL, "a loopback group merges through l5dh_merge_all");
   int r;
-  if ((r = merge_export(c))) return r;
+  if ((r = merge_export(c, mode))) return r;
   if ((r = merge_collectives(&c, 1, mode))) return r;
   return merge_finish(c, mode, out, counts_out, totals_out, first, count);
 }
@@ -1534,7 +1562,7 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
   int r;
   for (int i = 0; i < n; ++i) {
     hipSetDevice(ctxs[i]->device);
-    if ((r = merge_export(ctxs[i]))) return r;
+    if ((r = merge_export(ctxs[i], mode))) return r;
   }
   if ((r = merge_collectives(ctxs, n, mode))) return r;
   for (int i = 0; i < n; ++i) {

@@ -124,13 +124,21 @@ constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, 
 
 struct Plan {
   uint32_t* tile_tot;      // [F]
+  uint32_t* enc_base;      // [F] (sparse export) the tile's first word in the unpacked encoding
   uint4* cold_item;        // [F] cold item -> {tile | CI_DIRTY, a0, a1, n0 | n1 << 16}: segment 0's
                            // key ranges (rec16) of the tile's halves
   uint2* split_item;       // [split items] {tile | half << 15, chunk} of big tiles
   uint32_t* hot_list;      // [F] big tiles
   uint8_t* tile_flags;     // [F] TF_*
-  uint32_t* header;        // [4] cold items, big tiles, (unused), split items; then per-workgroup counts
+  uint32_t* header;        // [4] cold items, big tiles, cold-item counter, split items; [4 + k B + b] per-workgroup
+                           // sums of quantity k (B = ceil(F / 1024) plan workgroups); [4 + 4 B] split-item
+                           // counter; [5 + 4 B] the unpacked encoding's words (sparse export)
 };
+__host__ __device__ constexpr uint32_t plan_header_words(uint32_t F) { return 6 + 4 * ((F + 1023) / 1024); }
+// Sparse export (the fleet merge's reduce-scatter): words a tile's rows may take in the
+// unpacked encoding -- a clean cold tile at most its records (<= 65535 per tile: no
+// escaped counts), a big or dirty tile two halves of 16 rows x 3596 words at most
+constexpr uint32_t ENC_HALF_CAP = 16u * 2u * NB + 16u;
 
 struct Outputs {
   Summary88* summ;         // nullable, index = series - first
@@ -139,6 +147,9 @@ struct Outputs {
   int64_t* totals;         // nullable, [count] exact sums (the fleet-merge export)
   uint32_t* words;         // nullable, [count] the fleet merge's encoding words per row: non-empty
                            // buckets + counts >= MERGE_CMAX (which take a second word)
+  uint32_t* enc;           // nullable: sparse export -- the rows' encodings (unpacked: at Plan::enc_base of
+                           // their tile) instead of dense rows (counts must be null, summ null)
+  uint32_t* roff;          // [count] with enc: each row's first word in enc
 };
 constexpr uint32_t MERGE_CMAX = 0x1FFFFFu;  // count field of a merge entry; CMAX marks an escaped count
 
@@ -177,7 +188,7 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 
 // ---- snapshot launchers (l5dh_snapshot.hip) ----
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
-                       const uint8_t* dirty, int direct_out, Plan plan, hipStream_t st);
+                       const uint8_t* dirty, int direct_out, int encode, Plan plan, hipStream_t st);
 // The accumulate launches take UPPER BOUNDS of their item counts (no host round
 // trip for the plan header): the kernels are persistent and read the exact counts
 // from plan.header on the device.  DEV_COUNT as a count: read it on the device.

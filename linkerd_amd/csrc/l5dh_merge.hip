@@ -61,6 +61,20 @@ __global__ __launch_bounds__(256) void k_menc(const int32_t* __restrict__ rows, 
   }
 }
 
+// The sparse export's rows (encoded at their tiles' places by the accumulate kernels)
+// packed in row order: one wave per row.
+__global__ __launch_bounds__(256) void k_mpack(const uint32_t* __restrict__ src, const uint32_t* __restrict__ roff,
+                                               const uint32_t* __restrict__ words, const uint64_t* __restrict__ offs,
+                                               uint32_t nrows, uint32_t* __restrict__ enc) {
+  const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const uint32_t n = words[r];
+  if (n == 0) return;
+  const uint32_t* a = src + roff[r];
+  uint32_t* o = enc + offs[r];
+  for (uint32_t i = lane_id(); i < n; i += 64) o[i] = a[i];
+}
+
 // One wave per series of the slice: the LDS row accumulates every source's entries
 // (a source's words are parsed 64 at a time; escape headers are rare, resolved by a
 // loop over their ballot), then the dense row, the total and the summary.
@@ -256,6 +270,13 @@ hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uin
 hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
   hipLaunchKernelGGL(k_menc, dim3((nrows + 3) / 4), dim3(256), 0, st, rows, nrows, offs, enc);
+  return hipGetLastError();
+}
+
+hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint32_t* words, const uint64_t* offs,
+                      uint32_t nrows, uint32_t* enc, hipStream_t st) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mpack, dim3((nrows + 3) / 4), dim3(256), 0, st, src, roff, words, offs, nrows, enc);
   return hipGetLastError();
 }
 

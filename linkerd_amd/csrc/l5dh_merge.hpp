@@ -20,6 +20,9 @@ struct MergeSources {  // the encodings of this rank's row slice, one per source
 hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
                        size_t* tmp_bytes, hipStream_t st);
 hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st);
+// the sparse export's row encodings (row r: words[r] words at src + roff[r]) packed at offs[r]
+hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint32_t* words, const uint64_t* offs,
+                      uint32_t nrows, uint32_t* enc, hipStream_t st);
 // offs[0..nrows) = exclusive prefix of words (a received slice); tmp from merge_count's query
 hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
                          hipStream_t st);

@@ -39,7 +39,7 @@ __device__ __forceinline__ uint32_t seg_key_count(const Segs& sg, int j, uint32_
 // in chunks of hot_chunk records) and stores its workgroup's item counts in
 // header[4 + k B + b]; k_plan_b scans those and writes the lists in tile order.
 struct PlanCls {
-  uint32_t ci, hot, si, h0;
+  uint32_t ci, hot, si, h0, ec;  // ec: the tile's words in the unpacked encoding (sparse export)
 };
 __device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t F, uint32_t t, uint32_t& tot,
                                                  int final_mode, uint32_t cold_limit, uint32_t hot_chunk) {
@@ -49,7 +49,7 @@ __device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t F, u
     h1 += seg_key_count(segs, j, F, 2 * t + 1);
   }
   tot = h0 + h1;
-  PlanCls r{0u, 0u, 0u, h0};
+  PlanCls r{0u, 0u, 0u, h0, 0u};
   if (tot > cold_limit) {
     r.hot = 1;
     r.si = (h0 + hot_chunk - 1) / hot_chunk + (h1 + hot_chunk - 1) / hot_chunk;
@@ -59,25 +59,31 @@ __device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t F, u
   return r;
 }
 
+__device__ __forceinline__ uint32_t enc_cap(const PlanCls& c, uint32_t tot, bool dirty) {
+  return (c.hot || dirty) ? 2u * ENC_HALF_CAP : tot + TILE;
+}
+
 __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
-                                                 uint32_t hot_chunk, Plan plan) {
-  __shared__ uint32_t red[3][17];
+                                                 uint32_t hot_chunk, const uint8_t* __restrict__ dirty, int encode,
+                                                 Plan plan) {
+  __shared__ uint32_t red[4][17];
   const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
-  PlanCls c{0u, 0u, 0u, 0u};
+  PlanCls c{0u, 0u, 0u, 0u, 0u};
   if (t < F) {
     uint32_t tot;
     c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
+    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0);
     plan.tile_tot[t] = tot;
   }
-  const uint32_t v[3] = {c.ci, c.hot, c.si};
+  const uint32_t v[4] = {c.ci, c.hot, c.si, c.ec};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < 4; ++k) {
     const uint32_t x = wave_sum((uint64_t)v[k]);
     if (lane == 0) red[k][w] = x;
   }
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 4) {
     uint32_t x = 0;
     for (int q = 0; q < 16; ++q) x += red[threadIdx.x][q];
     plan.header[4 + threadIdx.x * gridDim.x + blockIdx.x] = x;
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int fina
 
 __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
                                                  uint32_t hot_chunk, const uint8_t* __restrict__ dirty, int direct_out,
-                                                 Plan plan) {
+                                                 int encode, Plan plan) {
   __shared__ uint4 lds4[17];
   __shared__ uint32_t base[4];
   __shared__ uint32_t nbig;
@@ -96,32 +102,35 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   {
     uint32_t x[4], tx[4];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) x[k] = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
-    x[3] = 0u;
+    for (int k = 0; k < 4; ++k) x[k] = threadIdx.x < blockIdx.x ? plan.header[4 + k * B + threadIdx.x] : 0u;
     block_excl_scan4<1024>(x, lds4, tx);
     if (threadIdx.x < 4) base[threadIdx.x] = tx[threadIdx.x];
     if (blockIdx.x == 0) {
       uint32_t y[4], ty[4];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
-      y[3] = 0u;
+      for (int k = 0; k < 4; ++k) y[k] = threadIdx.x < B ? plan.header[4 + k * B + threadIdx.x] : 0u;
       block_excl_scan4<1024>(y, lds4, ty);
       if (threadIdx.x == 0) {  // header: cold items, big tiles, cold-item counter, split items
         plan.header[0] = ty[0];
         plan.header[1] = ty[1];
         plan.header[2] = 0u;
         plan.header[3] = ty[2];
-        plan.header[4 + 3 * B] = 0u;  // split-item counter
+        plan.header[4 + 4 * B] = 0u;   // split-item counter
+        plan.header[5 + 4 * B] = ty[3];  // the unpacked encoding's words
       }
     }
   }
   __syncthreads();
   const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
-  PlanCls c{0u, 0u, 0u, 0u};
+  PlanCls c{0u, 0u, 0u, 0u, 0u};
   uint32_t tot = 0;
-  if (t < F) c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
-  uint32_t pv[4] = {c.ci, c.hot, c.si, 0u}, ptot[4];
+  if (t < F) {
+    c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
+    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0);
+  }
+  uint32_t pv[4] = {c.ci, c.hot, c.si, c.ec}, ptot[4];
   block_excl_scan4<1024>(pv, lds4, ptot);
+  if (encode && t < F) plan.enc_base[t] = base[3] + pv[3];
   const uint32_t ca = base[0] + pv[0];
   const uint32_t xa = base[1] + pv[1];
   uint32_t sa = base[2] + pv[2];
@@ -342,6 +351,7 @@ __device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t 
 // per series emits the dense row and the summary (the series' exact sum is its
 // sumfix: the value sums were folded at ingest).  The midpoints are staged once;
 // each wave clears its series' LDS rows right after emitting them.
+template <bool ENCODE>  // the fleet merge's sparse export (out.enc: row encodings, no rows or summaries)
 __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                           uint32_t cold_arg, int final_mode, int reset) {
   constexpr int NT = 1024;
@@ -370,7 +380,8 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   // Every load is unconditional (clamped indices, masked where used), so no wait for
   // it is placed before the emission.
   const bool one = segs.n == 1;
-  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0;
+  constexpr bool encode = ENCODE;
+  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0, eb = 0;
   bool dirty = false;
   int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
@@ -392,7 +403,9 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
       x1 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n1 ? a1 + 8 * g : a1));
     }
     fraw = st.sumfix[min(t * TILE + (threadIdx.x & (TILE - 1)), st.S - 1)];
+    if (encode) eb = plan.enc_base[t];
   };
+  __shared__ uint32_t rwl[TILE];  // (sparse export) words of the tile's rows
   const uint4* __restrict__ citem = plan.cold_item;
   const uint32_t last = cold_items - 1u;
   // Items: a workgroup's first two are blockIdx.x and blockIdx.x + G; the rest come from
@@ -408,7 +421,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   uint4 cn = citem[min(item1, last)];  // the next item's entry, in flight
   __syncthreads();
   for (int par = 0; item < cold_items; par ^= 1) {
-    const uint32_t tc = t;
+    const uint32_t tc = t, ebc = eb;
     const bool dc = dirty;
     if (threadIdx.x < TILE) {
       const uint32_t s = tc * TILE + threadIdx.x;
@@ -447,7 +460,40 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
                         s0 + TILE <= st.S && (oi0 & 1u) == 0u;
-    for (int loc = w; loc < TILE; loc += NT / 64) {
+    if (encode) {
+      // (a whole-range resetting export) each row's words, then its entries at its
+      // place in the tile's range of the unpacked encoding (rows in order)
+      for (int loc = w; loc < TILE; loc += NT / 64) {
+        const uint32_t s = s0 + loc;
+        uint32_t nw = 0;
+        if (s < st.S)
+          nw = dc ? row_words(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}})
+                  : row_words(SrcLds16{hist + loc * CROW});
+        if (lane == 0) rwl[loc] = nw;
+      }
+      __syncthreads();
+      for (int loc = w; loc < TILE; loc += NT / 64) {
+        const uint32_t s = s0 + loc;
+        if (s < st.S) {
+          uint32_t at = ebc;
+          for (int l = 0; l < loc; ++l) at += rwl[l];
+          if (dc)
+            row_encode(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}},
+                       out.enc, at);
+          else
+            row_encode(SrcLds16{hist + loc * CROW}, out.enc, at);
+          if (lane == 0) {
+            const uint32_t oi = s - out.first;
+            out.roff[oi] = at;
+            out.words[oi] = rwl[loc];
+            if (out.totals) out.totals[oi] = fixl[loc] + (dc ? st.total[s] : 0);
+          }
+        }
+        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);  // this wave's row, cleared for the next item
+        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    for (int loc = w; !encode && loc < TILE; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
@@ -645,7 +691,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
   auto hist_add = [&](uint32_t loc, uint32_t b) { atomicAdd(&hist[(loc & 15u) * HROW + b], 1u); };
   // items: blockIdx.x first, then from a counter (G, G + 1, ...) as workgroups finish
   __shared__ uint32_t s_item;
-  uint32_t* const ctr = plan.header + 4 + 3 * ((F + 1023) / 1024);  // zeroed by k_plan_b
+  uint32_t* const ctr = plan.header + 4 + 4 * ((F + 1023) / 1024);  // zeroed by k_plan_b
   for (uint32_t item = blockIdx.x; item < nitems; item = s_item) {
     const uint2 it = plan.split_item[item];
     const uint32_t t = it.x & 0x7FFFu, half = (it.x >> 15) & 1u;
@@ -734,6 +780,7 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
 __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables tb, Outputs out, int final_mode,
                                                    int reset, int direct_out) {
   const uint32_t nv = 2 * plan.header[1];  // persistent: (big tile, half) pairs
+  __shared__ uint32_t rw16[16];  // (sparse export) words of the half's rows
   for (uint32_t vb = blockIdx.x; vb < nv; vb += gridDim.x) {
     const uint32_t t = plan.hot_list[vb >> 1];
     const uint32_t half = vb & 1u;
@@ -741,6 +788,29 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t s = t * TILE + 16 * half + w;
+    if (out.enc) {
+      // sparse export (the rows are the state rows: no direct_out): each row's words, then
+      // its entries in the half's range of the tile's unpacked encoding
+      const SrcRow32 src{st.counts + (size_t)s * ROW};
+      const uint32_t nw = s < st.S ? row_words(src) : 0u;
+      if (lane == 0) rw16[w] = nw;
+      __syncthreads();
+      if (s < st.S) {
+        uint32_t at = plan.enc_base[t] + half * ENC_HALF_CAP;
+        for (int l = 0; l < w; ++l) at += rw16[l];
+        row_encode(src, out.enc, at);
+        if (lane == 0) {
+          const uint32_t oi = s - out.first;
+          out.roff[oi] = at;
+          out.words[oi] = nw;
+          if (out.totals) out.totals[oi] = st.total[s] + st.sumfix[s];
+          st.sumfix[s] = 0;
+        }
+      }
+      if (threadIdx.x == 0 && half == 0) st.dirty[t] = 0;
+      __syncthreads();  // rw16 read before the next pair's
+      continue;
+    }
     if (s < st.S) {
       int64_t total = st.total[s] + st.sumfix[s];
       if (final_mode) {
@@ -833,8 +903,11 @@ int num_cus() {
 }  // namespace
 
 hipError_t set_snapshot_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)ACC_COLD_LDS);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_cold_p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)ACC_COLD_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
@@ -844,11 +917,12 @@ hipError_t set_snapshot_attributes() {
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
-                       const uint8_t* dirty, int direct_out, Plan plan, hipStream_t st) {
-  const uint32_t B = (F + 1023) / 1024;  // header holds 4 + 3 B words (l5dh_engine.cpp)
-  hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, plan);
+                       const uint8_t* dirty, int direct_out, int encode, Plan plan, hipStream_t st) {
+  const uint32_t B = (F + 1023) / 1024;  // header holds plan_header_words(F) words
+  hipLaunchKernelGGL(k_plan_a, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty, encode,
+                     plan);
   hipLaunchKernelGGL(k_plan_b, dim3(B), dim3(1024), 0, st, segs, F, final_mode, cold_limit, hot_chunk, dirty,
-                     direct_out, plan);
+                     direct_out, encode, plan);
   return hipGetLastError();
 }
 
@@ -865,8 +939,12 @@ hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State st
   // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
   // may be DEV_COUNT (read on the device)
   const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
-  hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
-                     cold_items, final_mode, reset);
+  if (out.enc)
+    hipLaunchKernelGGL(k_accum_cold_p<true>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
+                       cold_items, final_mode, reset);
+  else
+    hipLaunchKernelGGL(k_accum_cold_p<false>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
+                       cold_items, final_mode, reset);
   return hipGetLastError();
 }
 

@@ -95,7 +95,8 @@ def test_loopback_multirank_merge(oracle, W, mode):
     slices of the sparse encoding, the size all-gather, the payload exchange, the
     local slice decoded in place, the totals' reduce-scatter -- or the dense
     all-reduce -- with S not divisible by W, an escaped count (> 2^21 - 1 samples of
-    one bucket on one rank) and two merge intervals through the same buffers."""
+    one bucket on one rank) and two merge intervals through the same buffers, the
+    second with kept state (dirty tiles) under new records."""
     from linkerd_amd.engine import HistogramEngine
     S = 4001
     engines = [HistogramEngine(S) for _ in range(W)]
@@ -108,7 +109,13 @@ def test_loopback_multirank_merge(oracle, W, mode):
             parts = []
             for r, e in enumerate(engines):
                 p = (series[r::W], vals[r::W])
-                e.ingest(*p)
+                if interval == 1:  # kept state: half folded by a non-resetting snapshot (dirty tiles)
+                    h = p[0].size // 2
+                    e.ingest(p[0][:h], p[1][:h])
+                    e.snapshot(reset=False)
+                    e.ingest(p[0][h:], p[1][h:])
+                else:
+                    e.ingest(*p)
                 parts.append(p)
             if interval == 0:  # series 17: one bucket past the encoding's count field, on the last rank
                 heavy = (np.full(2_100_000, 17, np.uint32), np.full(2_100_000, 3.0, np.float32))
