@@ -544,10 +544,6 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
     HIPCHK(c, launch_ingest(a, 1, c->stream));
   }
   {
-    KTimer kt(c, L5DH_K_SCAN);
-    HIPCHK(c, launch_ingest(a, 2, c->stream));
-  }
-  {
     KTimer kt(c, L5DH_K_BIN2);
     HIPCHK(c, launch_ingest(a, 3, c->stream));
   }

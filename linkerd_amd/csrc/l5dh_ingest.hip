@@ -14,8 +14,8 @@
 //   k_rfix1    a run that did not fit its region -> exact regions from the cursors
 //              and a second k_rbin1w pass (launched always, it exits unless needed);
 //              the direct keys' ranges; the invalid-id count to the host
-//   k_rplan2a/b level-2 regions of the other keys; level-2 items (16K records of a
-//              super-tile's level-1 region)
+//              (k_rplan1 also plans the level-2 regions of the other keys, k_rfix1 the
+//              level-2 items: 16K records of a super-tile's level-1 region)
 //   k_rbin2    level 2: an item LDS-sorted by key into 16-bit records (series in
 //              tile | bucket) in its keys' regions; value sums folded into sumfix
 //   k_rfix2a/b exact key counts -> kprev (the next batch's prediction); overflow ->
@@ -120,10 +120,10 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
 // Level-1 plan, one workgroup.  Thread j owns tiles [32 j, 32 j + 32) (F <= 32768)
 // and bin j.  Direct tiles: the <= dmax tiles with the most estimated records, at
 // least max(thr_min, 2^k), k the smallest power keeping <= dmax of them.
-__global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
+__global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, uint32_t* __restrict__ kest,
                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
-                                                 size_t cap32, size_t dlim16, uint32_t thr_min, uint32_t dmax,
-                                                 uint32_t pct) {
+                                                 size_t cap32, size_t dlim16, size_t cap16, uint32_t thr_min,
+                                                 uint32_t dmax, uint32_t pct) {
   __shared__ uint32_t lh[33];
   __shared__ uint32_t sthr;
   __shared__ uint4 lds4[17];
@@ -287,7 +287,69 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
     hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
-    hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);
+    hdr[H_D16] = (uint32_t)dlim16;  // level 2's regions: above the direct keys' space, whatever they take
+  }
+  // Level-2 regions of this thread's non-direct keys [64 j, 64 j + 64) (the same capacity
+  // rule; exact ones after an overflow: k_rfix2), from dlim16 up (so they do not depend on
+  // what the direct keys take); kest zeroed for the next batch
+  {
+    const uint32_t k0 = 2u * t0;
+    auto key_caps = [&](int h, uint32_t (&c)[16]) {  // keys k0 + 16 h + q: 16-B loads, a ragged end word by word
+      uint32_t e[16], p[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t k = k0 + 16u * h + 4u * g;
+        uint4 x = make_uint4(0u, 0u, 0u, 0u), y = x;
+        if (k + 3 < L.K) {
+          x = *reinterpret_cast<const uint4*>(kest + k);
+          y = *reinterpret_cast<const uint4*>(kprev + k);
+        } else {
+          if (k < L.K) { x.x = kest[k]; y.x = kprev[k]; }
+          if (k + 1 < L.K) { x.y = kest[k + 1]; y.y = kprev[k + 1]; }
+          if (k + 2 < L.K) { x.z = kest[k + 2]; y.z = kprev[k + 2]; }
+        }
+        e[4 * g] = x.x; e[4 * g + 1] = x.y; e[4 * g + 2] = x.z; e[4 * g + 3] = x.w;
+        p[4 * g] = y.x; p[4 * g + 1] = y.y; p[4 * g + 2] = y.z; p[4 * g + 3] = y.w;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t k = k0 + 16u * h + (uint32_t)q;
+        const bool mine = k < L.K && !((dbits >> ((16 * h + q) >> 1)) & 1u);
+        c[q] = mine ? rcap((double)p[q], (double)e[q], s, exact, 32.0, 8, pct) : 0u;
+      }
+    };
+    uint64_t sum = 0;
+    for (int h = 0; h < 4; ++h) {
+      uint32_t c[16];
+      key_caps(h, c);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum += c[q];
+    }
+    uint64_t tot;
+    uint64_t base = (uint64_t)dlim16 + block_excl_scan64(sum, l64, &tot);
+    for (int h = 0; h < 4; ++h) {
+      uint32_t c[16];
+      key_caps(h, c);  // (the same loads again: L2 hits)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t k = k0 + 16u * h + (uint32_t)q;
+        if (k < L.K && !((dbits >> ((16 * h + q) >> 1)) & 1u)) {  // (direct keys: k_rfix1)
+          uint32_t cq = c[q];
+          if (base + cq + 64 > cap16) cq = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
+          meta[L.kbase() + k] = (uint32_t)base;
+          meta[L.kcap() + k] = cq;
+          meta[L.kcnt() + k] = 0u;
+        }
+        base += c[q];
+      }
+    }
+    __syncthreads();  // every thread's estimates are read
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const uint32_t k = k0 + 4u * g;
+      if (k + 3 < L.K) *reinterpret_cast<uint4*>(kest + k) = make_uint4(0u, 0u, 0u, 0u);
+      else for (uint32_t i = k; i < L.K; ++i) kest[i] = 0u;
+    }
   }
 }
 
@@ -326,7 +388,11 @@ constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 constexpr int NT1 = L5DH_RBIN1_NT;  // (development builds may set 1024: 24 slots per thread)
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
+#ifdef L5DH_DSUM64
+  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 8;
+#else
   return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
+#endif
 }
 
 template <int NT, int CH>
@@ -347,7 +413,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
+#ifdef L5DH_DSUM64
+  unsigned long long* dsum = reinterpret_cast<unsigned long long*>(lut2 + LUT2_N);  // [DSUM_N] u64 sums
+#else
   uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
+#endif
   __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
@@ -434,9 +504,12 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         }
         uint2 dv[4], lv[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
-          lv[q] = lut2[lut2_index(pl[q])];                      // (used by direct slots only)
+        for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // the bucket LUT, read by the direct slots only
+          lv[q] = make_uint2(0u, 0u);
+          if (__builtin_amdgcn_ubfe(dv[q].x, __builtin_amdgcn_ubfe(sv[g + q], TILE_SHIFT, 5), 1) != 0u)
+            lv[q] = lut2[lut2_index(pl[q])];
         }
         uint32_t rc4[4];
 #pragma unroll
@@ -460,6 +533,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
 #if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only: no value sums
+#elif defined(L5DH_DSUM64)
+          if (direct && !esc && p != 0u && pass == 0)
+            atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], (unsigned long long)p);
 #elif defined(L5DH_EXP) && (L5DH_EXP & 2)  // timing only: value sums without the wrap check
           if (direct && !esc && p != 0u && pass == 0) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
 #else
@@ -599,7 +675,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     // the slab's direct value sums (every wave's adds are in: the last barrier) into sumfix
     const uint32_t* dl = meta + L.dlist();
     for (uint32_t i = threadIdx.x; i < ND * TILE; i += NT) {
-      const uint32_t v = dsum[i];
+      const unsigned long long v = dsum[i];
       const uint32_t s = dl[i / TILE] * TILE + (i & (TILE - 1));
       if (v && s < S) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), (unsigned long long)v);
     }
@@ -610,7 +686,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 // ------------------------------------------------------------------------
 // After level 1 (one workgroup, thread = bin): exact bin totals, the direct keys'
 // ranges, and on an overflow exact regions for the redo pass (super-tile bins in
-// rec32, direct half-bins in rec16 from 0; H_D16 = their total).
+// rec32, direct half-bins in rec16 from 0), and the level-2 items per super-tile.
 __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict__ meta, const uint32_t* __restrict__ err,
                                                 uint32_t* __restrict__ err_host) {
   __shared__ uint32_t lds[17];
@@ -640,23 +716,24 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
     meta[L.bcap() + b] = round_up(c, stb ? 4 : 8);
     meta[L.bcnt() + b] = 0u;
   }
+  // level-2 items: ITEM2 level-1 records of a super-tile's region (k_rbin2 finds an
+  // item's super-tile in istart); the totals are exact either way
+  uint32_t all;
+  const uint32_t is = block_excl_scan<1024>(stb ? (c + ITEM2 - 1) / ITEM2 : 0u, lds, &all);
+  if (stb) meta[L.istart() + b] = is;
   __syncthreads();  // every thread has read H_OV1
   if (b == 0) {
+    meta[L.istart() + FS] = all;
+    hdr[H_ITEMS] = all;
+    hdr[H_OV2] = 0u;
+    hdr[H_REDO2] = 0u;
     hdr[H_REDO1] = ov;
     hdr[H_OV1] = 0u;
-    if (ov) {
-      hdr[H_NOVR1] += 1u;
-      hdr[H_D16] = t16;
-    }
+    if (ov) hdr[H_NOVR1] += 1u;
   }
 }
 
 // ------------------------------------------------------------------------
-// Level-2 plan over ceil(2F / 1024) workgroups, key k = 1024 b + thread (coalesced):
-// k_rplan2a sizes the regions of the non-direct keys and sums them per workgroup;
-// k_rplan2b adds the earlier workgroups' sums, scans, and clamps a region that would
-// pass the buffer's end (its runs overflow and level 2 is redone exactly); its
-// workgroup 0 also plans the level-2 items (16K records of a super-tile's region).
 __device__ __forceinline__ bool tile_direct(const uint32_t* __restrict__ meta, const MetaLayout& L, uint32_t t) {
   return (meta[L.dbits() + (t >> 5)] >> (t & 31u)) & 1u;
 }
@@ -671,70 +748,6 @@ __device__ __forceinline__ uint64_t wsum_before(const uint64_t* __restrict__ ws,
   for (int q = 0; q < 16; ++q) r += red[q];
   __syncthreads();
   return r;
-}
-
-__global__ __launch_bounds__(1024) void k_rplan2a(size_t n, uint32_t F, uint32_t* __restrict__ kest,
-                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
-                                                  uint32_t pct) {
-  __shared__ uint64_t red[16];
-  const MetaLayout L = meta_layout(F);
-  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
-  const bool exact = m == n;
-  const double s = m ? (double)n / (double)m : 1.0;
-  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
-  uint32_t cap = 0;
-  if (k < L.K) {
-    const uint32_t e = kest[k];
-    if (e) kest[k] = 0;  // ready for the next batch
-    if (!tile_direct(meta, L, k >> 1)) {
-      cap = rcap((double)kprev[k], (double)e, s, exact, 32.0, 8, pct);
-      meta[L.kcap() + k] = cap;
-    }
-  }
-  const uint64_t w = wave_sum((uint64_t)cap);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int q = 0; q < 16; ++q) t += red[q];
-    reinterpret_cast<uint64_t*>(meta + L.wsum())[blockIdx.x] = t;
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restrict__ meta, size_t cap16) {
-  __shared__ uint64_t red[16];
-  __shared__ uint64_t l64[17];
-  __shared__ uint32_t lds[17];
-  const MetaLayout L = meta_layout(F);
-  uint32_t* hdr = meta + L.hdr();
-  const uint64_t before = wsum_before(reinterpret_cast<const uint64_t*>(meta + L.wsum()), blockIdx.x, red);
-  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
-  const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
-  uint32_t cap = mine ? meta[L.kcap() + k] : 0u;
-  uint64_t total;
-  // (level-2 regions follow the direct keys' regions of rec16)
-  const uint64_t base = hdr[H_D16] + before + block_excl_scan64((uint64_t)cap, l64, &total);
-  if (mine) {
-    if (base + cap + 64 > cap16) cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
-    meta[L.kbase() + k] = (uint32_t)base;
-    meta[L.kcap() + k] = cap;
-    meta[L.kcnt() + k] = 0u;
-  }
-  if (blockIdx.x != 0) return;  // (workgroup-uniform)
-  // level-2 items of super-tile j = thread (k_rbin2 finds an item's super-tile in istart)
-  const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
-  const uint32_t j = threadIdx.x;
-  const uint32_t tot = j < FS ? meta[L.btot() + j] : 0u;
-  const uint32_t ni = (tot + ITEM2 - 1) / ITEM2;
-  uint32_t all;
-  const uint32_t is = block_excl_scan<1024>(ni, lds, &all);
-  if (j < FS) meta[L.istart() + j] = is;
-  if (j == 0) {
-    meta[L.istart() + FS] = all;
-    hdr[H_ITEMS] = all;
-    hdr[H_OV2] = 0u;
-    hdr[H_REDO2] = 0u;
-  }
 }
 
 // ------------------------------------------------------------------------
@@ -1033,7 +1046,7 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
       hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
                          a.kest);
       hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
-                         a.dlim16, a.thr_min, a.dmax, a.pct);
+                         a.dlim16, a.cap16, a.thr_min, a.dmax, a.pct);
       break;
     case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
       for (int pass = 0; pass < 2; ++pass) {
@@ -1042,12 +1055,8 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
         if (pass == 0) hipLaunchKernelGGL(k_rfix1, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.err, a.err_host);
       }
       break;
-    case 2: {  // level-2 plan
-      const uint32_t B = (K + 1023) / 1024;  // <= 64 (wsum)
-      hipLaunchKernelGGL(k_rplan2a, dim3(B), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.pct);
-      hipLaunchKernelGGL(k_rplan2b, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.cap16);
+    case 2:  // (the level-2 plan is made by k_rplan1 and k_rfix1)
       break;
-    }
     default: {  // level 2, its fix-up, the redo pass
       const uint32_t B = (K + 1023) / 1024;
       for (int pass = 0; pass < 2; ++pass) {

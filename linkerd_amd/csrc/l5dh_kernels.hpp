@@ -35,6 +35,7 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 // LDS bytes of the accumulate kernels: 32 u16-packed rows + the tile's sumfix + the
 // bucket midpoints (cold tiles), 16 u32 rows (big half-tiles)
 constexpr size_t ACC_COLD_LDS = (size_t)TILE * CROW * 4 + TILE * 8 + ROW * 4;
+constexpr size_t ACC_COLDH_LDS = (size_t)16 * CROW * 4 + 16 * 8 + ROW * 4;  // half-tile cold items
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4;
 // k_fold1 (samples, not records): u32 rows of 16 series or u16-packed rows of 32, lane-private
 // u64 value sums, the bucket LUT
@@ -57,7 +58,11 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 // records: [kbase[k], kbase[k] + kcnt[k]) of rec16 -- written by level 1 when tile
 // t is a direct tile of the batch (regions [0, H_D16)), by level 2 otherwise.
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
+#ifdef L5DH_DSUM64  // (development A/B: u64 LDS value sums of the direct series, half as many direct tiles)
+constexpr int DIRECT_MAX = 127;
+#else
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
+#endif
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
 constexpr uint32_t ITEM2 = 16384;   // level-1 records per level-2 item
 struct MetaLayout {
@@ -176,7 +181,8 @@ struct IngestArgs {
   uint32_t pct;            // region capacity scale, percent (100: as predicted)
   bool vec;                // 16-B aligned inputs
 };
-// Stages: 0 = sample + level-1 plan + level 1 (+ redo), 1 = level-2 plan + level 2 (+ redo).
+// Stages: 0 = sample + plans (level-1 bins and direct tiles, level-2 regions), 1 = level 1
+// (+ its fix-up: exact totals, level-2 items; + redo), 3 = level 2 (+ fix-up, redo).
 hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st);
 hipError_t set_ingest_attributes();
 

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   };
   __shared__ uint32_t rwl[TILE];  // (sparse export) words of the tile's rows
   const uint4* __restrict__ citem = plan.cold_item;
-  const uint32_t last = cold_items - 1u;
+  const uint32_t last = cold_items ? cold_items - 1u : 0u;  // (clamped prefetch indices stay in the list)
   // Items: a workgroup's first two are blockIdx.x and blockIdx.x + G; the rest come from
   // a counter (2G, 2G + 1, ... in the order workgroups ask), so a workgroup that starts
   // late -- its CU held by a k_accum_split workgroup -- takes fewer.  Each index is asked
@@ -545,6 +545,157 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
       s_next[par ^ 1] = asked;
     }
     __syncthreads();  // rows cleared, fixl consumed, the next index visible
+    item = item1;
+    item1 = item2;
+  }
+}
+
+// k_accum_cold_h: the cold tiles as half-tile items -- 16 series in one u16-packed LDS
+// histogram (57.6 KB), 512-thread workgroups, two per CU, so one workgroup counts
+// while the other emits its rows (k_accum_cold_p keeps one tile in flight per CU).
+// Item i is half i & 1 of cold item i >> 1.  Not for the sparse export.
+constexpr int HSER = 16;
+__global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, State st, Tables tb, Outputs out,
+                                                         uint32_t cold_arg, int final_mode, int reset) {
+  constexpr int NT = 512;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t cold_tiles = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
+  const uint32_t nitems = 2u * cold_tiles;
+  uint32_t* hist = smem;                                             // [16][900] u16 pairs
+  int64_t* fixl = reinterpret_cast<int64_t*>(smem + HSER * CROW);    // [16] sumfix of the item's series
+  int32_t* midl = reinterpret_cast<int32_t*>(fixl + HSER);           // [NB] bucket midpoints
+  const int w = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const bool keep = !(final_mode && reset);
+  const uint32_t F = st.F;
+  Tables tbl = tb;
+  tbl.mid = midl;
+  auto hist_add = [&](uint32_t loc, uint32_t b) {
+    atomicAdd(&hist[(loc & (HSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+  };
+  {
+    uint4* p = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < HSER * CROW / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
+  }
+  // the next item's entry is loaded one item ahead; its sumfix and (one pending
+  // segment) each thread's first 16-B group during this item's emission
+  const bool one = segs.n == 1;
+  uint32_t t = 0, a = 0, nn = 0, hf = 0;
+  bool dirty = false;
+  int64_t fraw = 0;
+  uint4 x0 = make_uint4(0u, 0u, 0u, 0u);
+  const uint16_t* const b16 = segs.rec16[0];
+  auto fetch = [&](uint4 ci, uint32_t half) {
+    asm volatile("" : "+v"(ci.x), "+v"(ci.y), "+v"(ci.z), "+v"(ci.w));
+    const uint32_t cx = __builtin_amdgcn_readfirstlane(ci.x), cw = __builtin_amdgcn_readfirstlane(ci.w);
+    t = cx & 0x7FFFu;
+    hf = half;
+    dirty = (cx & CI_DIRTY) != 0u;
+    a = __builtin_amdgcn_readfirstlane(half ? ci.z : ci.y);
+    nn = half ? cw >> 16 : cw & 0xFFFFu;
+    if (one) {
+      const uint32_t g = threadIdx.x;
+      x0 = *reinterpret_cast<const uint4*>(b16 + (8 * g < nn ? a + 8 * g : a));
+    }
+    fraw = st.sumfix[min(t * TILE + HSER * half + (threadIdx.x & (HSER - 1)), st.S - 1)];
+  };
+  const uint4* __restrict__ citem = plan.cold_item;
+  const uint32_t last = cold_tiles ? cold_tiles - 1u : 0u;
+  // items: blockIdx.x, blockIdx.x + G, then from the counter, asked two items ahead
+  __shared__ uint32_t s_next[2];
+  uint32_t* const ctr = plan.header + 2;  // zeroed by k_plan_b
+  const uint32_t G2 = 2u * gridDim.x;
+  if (threadIdx.x == 0) s_next[0] = G2 + atomicAdd(ctr, 1u);
+  uint32_t item = blockIdx.x, item1 = blockIdx.x + gridDim.x;
+  if (item < nitems) fetch(citem[item >> 1], item & 1u);
+  uint4 cn = citem[min(item1 >> 1, last)];
+  __syncthreads();
+  for (int par = 0; item < nitems; par ^= 1) {
+    const uint32_t tc = t, hc = hf;
+    const bool dc = dirty;
+    if (threadIdx.x < HSER) {
+      const uint32_t s = tc * TILE + HSER * hc + threadIdx.x;
+      const int64_t f = s < st.S ? fraw : 0;
+      fixl[threadIdx.x] = f;
+      if (f) st.sumfix[s] = 0;
+    }
+    if (one) {
+      const uint32_t g0 = (nn + 7) / 8;
+      const uint4* p0 = reinterpret_cast<const uint4*>(b16 + a);
+      uint4 x = x0;
+      for (uint32_t g = threadIdx.x; g < g0; g += NT) {
+        const uint4 cx = x;
+        const uint32_t gn = g + NT;
+        x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
+        count16(cx, min(8u, nn - 8 * g), hist_add);
+      }
+    } else {
+      for (int j = 0; j < segs.n; ++j) {
+        const KeyRange r = seg_key(segs, j, F, tc, hc);
+        const uint32_t n = r.e - r.a, g0 = (n + 7) / 8;
+        const uint4* p = reinterpret_cast<const uint4*>(r.r16 + r.a);
+        for (uint32_t g = threadIdx.x; g < g0; g += NT) count16(p[g], min(8u, n - 8 * g), hist_add);
+      }
+    }
+    __syncthreads();  // counts complete; fixl visible
+    fetch(cn, item1 & 1u);  // (past the last item: a harmless refetch)
+    const uint32_t item2 = s_next[par];
+    cn = citem[min(item2 >> 1, last)];
+    uint32_t asked = 0;
+    if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);
+    const uint32_t s0 = tc * TILE + HSER * hc;
+    const uint32_t oi0 = s0 - out.first;
+    const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + HSER <= out.count &&
+                        s0 + HSER <= st.S && (oi0 & 1u) == 0u;
+    for (int loc = w; loc < HSER; loc += NT / 64) {
+      const uint32_t s = s0 + loc;
+      const uint32_t* row = hist + loc * CROW;
+      if (s < st.S) {
+        if (linear) {
+          const int ng = lane_groups(lane);
+          uint32_t g[9], nw = 0;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) {
+            g[q] = 0u;
+            if (q < ng) {
+              const uint4 v = SrcLds16{row}.get4(28 * lane + 4 * q);
+              g[q] = sum4(v);
+              nw += merge_words4(v);
+            }
+          }
+          put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
+          wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
+        } else {
+          emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
+        }
+      }
+      if (!linear) {
+        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
+        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    if (linear) {
+      __syncthreads();  // the summaries have read the rows
+      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
+      constexpr int NCH = HSER * NB / 4;
+      for (int c = threadIdx.x; c < NCH; c += NT) {
+        const int e0 = 4 * c;
+        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
+        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
+        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
+        const uint32_t x = *p0, y = *p1;
+        *p0 = 0u;
+        *p1 = 0u;
+        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+      }
+    }
+    if (threadIdx.x == 0) {
+      st.dirty[tc] = keep ? 1 : 0;
+      s_next[par ^ 1] = asked;
+    }
+    __syncthreads();
     item = item1;
     item1 = item2;
   }
@@ -909,6 +1060,9 @@ hipError_t set_snapshot_attributes() {
   e = hipFuncSetAttribute((const void*)k_accum_cold_p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)ACC_COLD_LDS);
   if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_accum_cold_h, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)ACC_COLDH_LDS);
+  if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FOLD16_LDS);
@@ -942,6 +1096,14 @@ hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State st
   if (out.enc)
     hipLaunchKernelGGL(k_accum_cold_p<true>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
+#ifndef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel)
+  else if (true) {
+    // half-tile items, two 512-thread workgroups per CU
+    const uint32_t g2 = std::min<uint32_t>(cold_items == DEV_COUNT ? 0xFFFFFFFFu : 2u * cold_items, 2u * (uint32_t)num_cus());
+    hipLaunchKernelGGL(k_accum_cold_h, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out, cold_items,
+                       final_mode, reset);
+  }
+#endif
   else
     hipLaunchKernelGGL(k_accum_cold_p<false>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
