@@ -532,7 +532,8 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   a.dlim16 = dlim16;
   a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
   const uint32_t FS = (c->F + 63) / 64;
-  a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 1 - FS) / 2);  // + the trash bin
+  // + the trash bin, below the hot bin's 8 rank replicas (l5dh_ingest.hip REP0)
+  a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 9 - FS) / 2);
   a.pct = c->region_pct;
   a.vec = vec;
   {
@@ -868,26 +869,27 @@ int merge_finish(l5dh_ctx* c, int mode, l5dh_summary* out, int32_t* counts_out, 
         drows = static_cast<int32_t*>(c->recv_counts.p);
       }
     }
-    MergeSources src{};
-    src.n = W;
-    uint64_t rat = 0;
+    // the received slices are contiguous in r_enc / r_words, source by source; this
+    // rank's own slice (not sent) is copied to its place there, and one scan of the
+    // [W][per] word counts gives every source's row offsets
     KTimer kt(c, L5DH_K_MERGE);
-    for (int q = 0; q < W; ++q) {
-      const bool local = q == c->rank && W > 1;
-      if (local) {  // this rank's own slice, in place
-        uint64_t a0 = 0;
-        for (int k = 0; k < q; ++k) a0 += c->m_to[k];
-        src.enc[q] = static_cast<const uint32_t*>(c->m_enc.p) + a0;
-        src.words[q] = static_cast<const uint32_t*>(c->m_words.p) + (size_t)q * per;
-      } else {
-        src.enc[q] = static_cast<const uint32_t*>(c->r_enc.p) + rat;
-        src.words[q] = static_cast<const uint32_t*>(c->r_words.p) + (size_t)q * per;
+    uint32_t* renc = static_cast<uint32_t*>(c->r_enc.p);
+    uint32_t* rwords = static_cast<uint32_t*>(c->r_words.p);
+    if (W > 1) {
+      uint64_t a0 = 0, rat = 0;
+      for (int k = 0; k < c->rank; ++k) {
+        a0 += c->m_to[k];
+        rat += c->m_from[k];
       }
-      uint64_t* o = static_cast<uint64_t*>(c->r_offs.p) + (size_t)q * per;
-      HIPCHK(c, merge_offsets(src.words[q], per, o, c->m_tmp.p, c->m_tmp_bytes, c->stream));
-      src.offs[q] = o;
-      rat += c->m_from[q];
+      if (c->m_to[c->rank])
+        HIPCHK(c, hipMemcpyAsync(renc + rat, static_cast<const uint32_t*>(c->m_enc.p) + a0, c->m_to[c->rank] * 4,
+                                 hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(rwords + (size_t)c->rank * per, static_cast<const uint32_t*>(c->m_words.p) + (size_t)c->rank * per,
+                               (size_t)per * 4, hipMemcpyDeviceToDevice, c->stream));
     }
+    uint64_t* roffs = static_cast<uint64_t*>(c->r_offs.p);
+    HIPCHK(c, merge_offsets(rwords, (uint32_t)((size_t)W * per), roffs, c->m_tmp.p, c->m_tmp_bytes, c->stream));
+    const MergeRecv src{renc, rwords, roffs, per, W};
     HIPCHK(c, merge_decode(src, n, static_cast<const int64_t*>(c->recv_totals.p), tables(c), drows, d_summ, c->stream));
     rows = drows;
     tots = static_cast<const int64_t*>(c->recv_totals.p);

@@ -1,8 +1,8 @@
 // l5dh_ingest.hip -- ingest-side kernels (Metric.Stat.add, batched): a two-level
 // partition of the COO batch into capacity-planned regions, with no counting pass.
 //
-//   k_rsample  2^20 sampled ids (runs of 64 at 2^14 evenly spaced places; every
-//              sample of a smaller batch) counted per (tile, half) key
+//   k_rsample  ids of 2^20 evenly spaced samples (every sample of a smaller batch)
+//              counted per (tile, half) key
 //   k_rplan1   this batch's direct tiles (the biggest estimated) and the level-1 bin
 //              regions (super-tiles; two half-bins per direct tile), sized from the
 //              previous batch's exact key counts and this batch's sample
@@ -14,8 +14,8 @@
 //   k_rfix1    a run that did not fit its region -> exact regions from the cursors
 //              and a second k_rbin1w pass (launched always, it exits unless needed);
 //              the direct keys' ranges; the invalid-id count to the host
-//              (k_rplan1 also plans the level-2 regions of the other keys, k_rfix1 the
-//              level-2 items: 16K records of a super-tile's level-1 region)
+//   k_rplan2a/b level-2 regions of the other keys (with the level-1 plan; k_rfix1
+//              plans the level-2 items: 16K records of a super-tile's level-1 region)
 //   k_rbin2    level 2: an item LDS-sorted by key into 16-bit records (series in
 //              tile | bucket) in its keys' regions; value sums folded into sumfix
 //   k_rfix2a/b exact key counts -> kprev (the next batch's prediction); overflow ->
@@ -98,15 +98,22 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
   const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
   const uint64_t per = (m + RS_WG - 1) / RS_WG;
   const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
-  for (uint64_t k = k0 + threadIdx.x; k < k1; k += 1024) {
-    // runs of 64 consecutive ids at 2^14 evenly spaced places (one coalesced 256-B read
-    // per wave, not one line per draw); every id when the batch is <= 2^20
-    const uint64_t i = m == n ? k : (k >> 6) * n / (m >> 6) + (k & 63u);
-    const uint32_t s = series[i];
-    if (s < S) {
-      const uint32_t key = s >> 4;
-      atomicAdd(&c[key >> 1], (key & 1u) ? 0x10000u : 1u);
+  // evenly spaced single draws (runs of consecutive ids misjudge a structured stream,
+  // e.g. C2's affine permutation), four per thread with their loads in flight together
+  for (uint64_t kb = k0; kb < k1; kb += 4 * 1024) {
+    uint32_t sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t k = kb + threadIdx.x + 1024u * u;
+      const uint64_t i = m == n ? k : k * n / m;
+      sv[u] = k < k1 ? series[i < n ? i : 0] : 0xFFFFFFFFu;
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (sv[u] < S) {
+        const uint32_t key = sv[u] >> 4;
+        atomicAdd(&c[key >> 1], (key & 1u) ? 0x10000u : 1u);
+      }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) {
@@ -120,10 +127,10 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
 // Level-1 plan, one workgroup.  Thread j owns tiles [32 j, 32 j + 32) (F <= 32768)
 // and bin j.  Direct tiles: the <= dmax tiles with the most estimated records, at
 // least max(thr_min, 2^k), k the smallest power keeping <= dmax of them.
-__global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, uint32_t* __restrict__ kest,
+__global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
-                                                 size_t cap32, size_t dlim16, size_t cap16, uint32_t thr_min,
-                                                 uint32_t dmax, uint32_t pct) {
+                                                 size_t cap32, size_t dlim16, uint32_t thr_min, uint32_t dmax,
+                                                 uint32_t pct) {
   __shared__ uint32_t lh[33];
   __shared__ uint32_t sthr;
   __shared__ uint4 lds4[17];
@@ -289,68 +296,6 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, uint32_t*
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)dlim16;  // level 2's regions: above the direct keys' space, whatever they take
   }
-  // Level-2 regions of this thread's non-direct keys [64 j, 64 j + 64) (the same capacity
-  // rule; exact ones after an overflow: k_rfix2), from dlim16 up (so they do not depend on
-  // what the direct keys take); kest zeroed for the next batch
-  {
-    const uint32_t k0 = 2u * t0;
-    auto key_caps = [&](int h, uint32_t (&c)[16]) {  // keys k0 + 16 h + q: 16-B loads, a ragged end word by word
-      uint32_t e[16], p[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t k = k0 + 16u * h + 4u * g;
-        uint4 x = make_uint4(0u, 0u, 0u, 0u), y = x;
-        if (k + 3 < L.K) {
-          x = *reinterpret_cast<const uint4*>(kest + k);
-          y = *reinterpret_cast<const uint4*>(kprev + k);
-        } else {
-          if (k < L.K) { x.x = kest[k]; y.x = kprev[k]; }
-          if (k + 1 < L.K) { x.y = kest[k + 1]; y.y = kprev[k + 1]; }
-          if (k + 2 < L.K) { x.z = kest[k + 2]; y.z = kprev[k + 2]; }
-        }
-        e[4 * g] = x.x; e[4 * g + 1] = x.y; e[4 * g + 2] = x.z; e[4 * g + 3] = x.w;
-        p[4 * g] = y.x; p[4 * g + 1] = y.y; p[4 * g + 2] = y.z; p[4 * g + 3] = y.w;
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t k = k0 + 16u * h + (uint32_t)q;
-        const bool mine = k < L.K && !((dbits >> ((16 * h + q) >> 1)) & 1u);
-        c[q] = mine ? rcap((double)p[q], (double)e[q], s, exact, 32.0, 8, pct) : 0u;
-      }
-    };
-    uint64_t sum = 0;
-    for (int h = 0; h < 4; ++h) {
-      uint32_t c[16];
-      key_caps(h, c);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) sum += c[q];
-    }
-    uint64_t tot;
-    uint64_t base = (uint64_t)dlim16 + block_excl_scan64(sum, l64, &tot);
-    for (int h = 0; h < 4; ++h) {
-      uint32_t c[16];
-      key_caps(h, c);  // (the same loads again: L2 hits)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t k = k0 + 16u * h + (uint32_t)q;
-        if (k < L.K && !((dbits >> ((16 * h + q) >> 1)) & 1u)) {  // (direct keys: k_rfix1)
-          uint32_t cq = c[q];
-          if (base + cq + 64 > cap16) cq = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
-          meta[L.kbase() + k] = (uint32_t)base;
-          meta[L.kcap() + k] = cq;
-          meta[L.kcnt() + k] = 0u;
-        }
-        base += c[q];
-      }
-    }
-    __syncthreads();  // every thread's estimates are read
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const uint32_t k = k0 + 4u * g;
-      if (k + 3 < L.K) *reinterpret_cast<uint4*>(kest + k) = make_uint4(0u, 0u, 0u, 0u);
-      else for (uint32_t i = k; i < L.K; ++i) kest[i] = 0u;
-    }
-  }
 }
 
 // ------------------------------------------------------------------------
@@ -383,9 +328,13 @@ constexpr int CHW = 24576;
 // cap16 < 2^32 - CHW - 1, so -(CHW + 1) never is one (0xFFFFFFFF is: base 0 at offset 1)
 constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 #ifndef L5DH_RBIN1_NT
-#define L5DH_RBIN1_NT 768
+#define L5DH_RBIN1_NT 1024
 #endif
-constexpr int NT1 = L5DH_RBIN1_NT;  // (development builds may set 1024: 24 slots per thread)
+constexpr int NT1 = L5DH_RBIN1_NT;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
+// The batch's hottest bin (H_HB0) is ranked on 8 replica counters (LDS words REP0 + (lane &
+// 7), past every bin: bins <= REP0 - 1) so its lanes spread over 8 addresses, and its run
+// is staged as the replicas' runs back to back (subb: the replicas' prefix).
+[[maybe_unused]] constexpr uint32_t REP0 = BIN1_BINS - 8;
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
 #ifdef L5DH_DSUM64
@@ -419,6 +368,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
 #endif
   __shared__ uint32_t nruns;
+#ifdef L5DH_HOTREP
+  __shared__ uint32_t subb[8];  // hot-bin replicas' stage prefix
+#endif
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
@@ -531,7 +483,12 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+#ifdef L5DH_HOTREP
+          const uint32_t ci = bn == hb0 ? REP0 + ((uint32_t)lane & 7u) : bn;
+          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + ci, 1u) | (bn << 15) | (((uint32_t)lane & 7u) << 25);
+#else
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
+#endif
 #if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only: no value sums
 #elif defined(L5DH_DSUM64)
           if (direct && !esc && p != 0u && pass == 0)
@@ -556,7 +513,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t wc0 = 0, wc1 = 0;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        const uint32_t b = pk[k] >> 15;
+        const uint32_t b = (pk[k] >> 15) & 1023u;
         const bool m0 = b == hb0, m1 = b == hb1;
         wc0 += (uint32_t)__popcll(__ballot(m0));
         wc1 += (uint32_t)__popcll(__ballot(m1));
@@ -568,7 +525,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t r0 = __builtin_amdgcn_readlane(base, 0), r1 = __builtin_amdgcn_readlane(base, 1);
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        const uint32_t b = pk[k] >> 15;
+        const uint32_t b = (pk[k] >> 15) & 1023u;
         const bool m0 = b == hb0, m1 = b == hb1;
         const unsigned long long x0 = __ballot(m0), x1 = __ballot(m1);
         if (m0) pk[k] |= r0 + mask_below(x0);
@@ -578,13 +535,29 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B1: counts complete
+#ifdef L5DH_HOTREP
+    const bool rep = !hotrank && hb0 < REP0;
+    uint32_t hotc = 0;  // the hot bin's records (its replicas' sum)
+    if (rep) {
+      const uint4 ra = *reinterpret_cast<const uint4*>(cnt + REP0), rb = *reinterpret_cast<const uint4*>(cnt + REP0 + 4);
+      hotc = ra.x + ra.y + ra.z + ra.w + rb.x + rb.y + rb.z + rb.w;
+      if (threadIdx.x == 0) {
+        subb[0] = 0; subb[1] = ra.x; subb[2] = ra.x + ra.y; subb[3] = ra.x + ra.y + ra.z;
+        const uint32_t a4 = ra.x + ra.y + ra.z + ra.w;
+        subb[4] = a4; subb[5] = a4 + rb.x; subb[6] = a4 + rb.x + rb.y; subb[7] = a4 + rb.x + rb.y + rb.z;
+      }
+    }
+    auto bcount = [&](uint32_t b, uint32_t c) { return rep ? (b == hb0 ? hotc : b >= REP0 ? 0u : c) : c; };
+#else
+    auto bcount = [&](uint32_t, uint32_t c) { return c; };
+#endif
     // run reservations: thread t -> bins t, t + NT, ... (the trash bin TB gets none)
     constexpr int RB = (BIN1_BINS + NT - 1) / NT;
     uint32_t rn[RB], rold[RB], rbase[RB], rcapv[RB];
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
-      rn[j] = rb_bin <= TB ? cnt[rb_bin] : 0u;  // records of the bin in this sub-chunk
+      rn[j] = rb_bin <= TB ? bcount(rb_bin, cnt[rb_bin]) : 0u;  // records of the bin in this sub-chunk
       rold[j] = rbase[j] = rcapv[j] = 0;
       if (rb_bin < TB && rn[j]) {
         rold[j] = atomicAdd(&bcnt[rb_bin], rn[j]);
@@ -602,6 +575,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t tl = 0, tr = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
+        c[q] = bcount(16u * lane + q, c[q]);
         tl += c[q];
         tr += c[q] ? 1u : 0u;
       }
@@ -626,8 +600,13 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     __syncthreads();  // B2: offsets, run ranks, heads; every slot-order record read
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
-      const uint32_t bin = pk[k] >> 15;
-      stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
+      const uint32_t bin = (pk[k] >> 15) & 1023u;
+#ifdef L5DH_HOTREP
+      const uint32_t sb = rep && bin == hb0 ? subb[pk[k] >> 25] : 0u;
+#else
+      const uint32_t sb = 0u;
+#endif
+      stage[(offr[bin] & 0xFFFFu) + sb + (pk[k] & 0x7FFFu)] = rec[k];
     }
     if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
       const uint32_t at = threadIdx.x * 64u;
@@ -748,6 +727,60 @@ __device__ __forceinline__ uint64_t wsum_before(const uint64_t* __restrict__ ws,
   for (int q = 0; q < 16; ++q) r += red[q];
   __syncthreads();
   return r;
+}
+
+// Level-2 regions over ceil(2F / 1024) workgroups, key k = 1024 b + thread (coalesced):
+// k_rplan2a sizes the regions of the non-direct keys (the previous batch's exact
+// counts and this batch's sample; zeroes the sample for the next batch) and sums them
+// per workgroup; k_rplan2b adds the earlier workgroups' sums, scans, and clamps a region
+// that would pass the buffer's end (its runs overflow; level 2 is redone exactly).
+// Regions start at H_D16 (above the direct keys' space), so they are planned with the
+// direct tiles, before level 1.
+__global__ __launch_bounds__(1024) void k_rplan2a(size_t n, uint32_t F, uint32_t* __restrict__ kest,
+                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
+                                                  uint32_t pct) {
+  __shared__ uint64_t red[16];
+  const MetaLayout L = meta_layout(F);
+  const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
+  const bool exact = m == n;
+  const double s = m ? (double)n / (double)m : 1.0;
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  uint32_t cap = 0;
+  if (k < L.K) {
+    const uint32_t e = kest[k];
+    if (e) kest[k] = 0;  // ready for the next batch
+    if (!tile_direct(meta, L, k >> 1)) {
+      cap = rcap((double)kprev[k], (double)e, s, exact, 32.0, 8, pct);
+      meta[L.kcap() + k] = cap;
+    }
+  }
+  const uint64_t w = wave_sum((uint64_t)cap);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int q = 0; q < 16; ++q) t += red[q];
+    reinterpret_cast<uint64_t*>(meta + L.wsum())[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restrict__ meta, size_t cap16) {
+  __shared__ uint64_t red[16];
+  __shared__ uint64_t l64[17];
+  const MetaLayout L = meta_layout(F);
+  const uint32_t* hdr = meta + L.hdr();
+  const uint64_t before = wsum_before(reinterpret_cast<const uint64_t*>(meta + L.wsum()), blockIdx.x, red);
+  const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
+  const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
+  uint32_t cap = mine ? meta[L.kcap() + k] : 0u;
+  uint64_t total;
+  const uint64_t base = hdr[H_D16] + before + block_excl_scan64((uint64_t)cap, l64, &total);
+  if (mine) {
+    if (base + cap + 64 > cap16) cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
+    meta[L.kbase() + k] = (uint32_t)base;
+    meta[L.kcap() + k] = cap;
+    meta[L.kcnt() + k] = 0u;
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1046,7 +1079,12 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
       hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
                          a.kest);
       hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
-                         a.dlim16, a.cap16, a.thr_min, a.dmax, a.pct);
+                         a.dlim16, a.thr_min, a.dmax, a.pct);
+      {  // level-2 regions of the non-direct keys
+        const uint32_t B = (K + 1023) / 1024;  // <= 64 (wsum)
+        hipLaunchKernelGGL(k_rplan2a, dim3(B), dim3(1024), 0, st, a.n, a.F, a.kest, a.kprev, a.meta, a.pct);
+        hipLaunchKernelGGL(k_rplan2b, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.cap16);
+      }
       break;
     case 1:  // level 1, its fix-up, the redo pass (exits at once unless needed)
       for (int pass = 0; pass < 2; ++pass) {
