@@ -77,9 +77,7 @@ enum {
                                   below 100 exercise that path (tests) and cost time, never results */
   L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
                                   every variant computes the same results; bit 0: one-tile folds in u16 bins;
-                                  bit 1: DMA copies of pinned host batches; bits 3:2: level-1 kernel (1: 16K-slot
-                                  sub-chunks, 2: 8K-slot sub-chunks two workgroups per CU); bit 4: cold tiles'
-                                  dense stores before their summaries) */
+                                  bit 1: DMA copies of pinned host batches; other bits are ignored) */
 };
 
 /* Fleet-merge modes for l5dh_merge */

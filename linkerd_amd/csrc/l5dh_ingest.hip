@@ -294,7 +294,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
     hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
-    hdr[H_D16] = (uint32_t)dlim16;  // level 2's regions: above the direct keys' space, whatever they take
+    hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
 }
 
@@ -323,6 +323,25 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
 // lut2 [1024] uint2, direct sums [255 x 32].
+#ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
+__device__ unsigned long long g_phase1[1024 * 8];
+#define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
+#define PH_MARK(k)                                 \
+  if (threadIdx.x == 0) {                          \
+    const unsigned long long ph_n = wall_clock64(); \
+    ph_acc[k] += ph_n - ph_t;                      \
+    ph_t = ph_n;                                   \
+  }
+#define PH_FLUSH                                                                   \
+  if (threadIdx.x == 0 && pass == 0) {                                             \
+    for (int k = 0; k < 4; ++k) g_phase1[blockIdx.x * 8 + k] += ph_acc[k];          \
+    g_phase1[blockIdx.x * 8 + 7] += 1;                                             \
+  }
+#else
+#define PH_INIT
+#define PH_MARK(k)
+#define PH_FLUSH
+#endif
 constexpr int CHW = 24576;
 // rdelta of a dropped run: a valid delta (run base - stage offset) lies in (-CHW, cap16),
 // cap16 < 2^32 - CHW - 1, so -(CHW + 1) never is one (0xFFFFFFFF is: base 0 at offset 1)
@@ -395,12 +414,18 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t lo = (uint32_t)((size_t)blockIdx.x * per);
   const uint32_t hi = (uint32_t)min((size_t)lo + per, n);
   bool bad = false;
+  PH_INIT
   for (uint32_t c0 = lo; c0 < hi; c0 += CH) {
     for (uint32_t wd = threadIdx.x; wd < CH / 32; wd += NT) heads[wd] = 0u;
     // records are staged in slot order first (the stage is free until the scatter), so
     // only their ranks and bins stay in registers while the sub-chunk is ranked
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
+#if defined(L5DH_EXP) && (L5DH_EXP & 16)  // timing only: every sub-chunk loads the slab's first (L2 hits)
+    const uint32_t cl = lo;
+#else
+    const uint32_t cl = c0;
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t sv[PH];
@@ -408,7 +433,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       if (full) {
 #pragma unroll
         for (int k = 0; k < PH / 4; ++k) {
-          const uint32_t base = c0 + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
+          const uint32_t base = cl + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
           const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
           const float4 f4 = *reinterpret_cast<const float4*>(values + base);
           sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
@@ -535,6 +560,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B1: counts complete
+    PH_MARK(0)
 #ifdef L5DH_HOTREP
     const bool rep = !hotrank && hb0 < REP0;
     uint32_t hotc = 0;  // the hot bin's records (its replicas' sum)
@@ -598,6 +624,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       rec[4 * kk] = v.x; rec[4 * kk + 1] = v.y; rec[4 * kk + 2] = v.z; rec[4 * kk + 3] = v.w;
     }
     __syncthreads();  // B2: offsets, run ranks, heads; every slot-order record read
+    PH_MARK(1)
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = (pk[k] >> 15) & 1023u;
@@ -630,6 +657,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B3: stage, group prefixes, deltas (every count read: cleared below)
+    PH_MARK(2)
     const uint32_t nst = offr[FS] >> 16;  // runs of super-tile bins (u32 records); the later runs are u16
 #pragma unroll
     for (int j = 0; j < RB; ++j)
@@ -641,7 +669,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
+#if defined(L5DH_EXP) && (L5DH_EXP & 32)  // timing only: no write-out stores
+      if (d == 0x12345u) {
+#else
       if (d != NODEST) {
+#endif
         if (run < nst)
           rec32[i + d] = stage[i];
         else
@@ -649,7 +681,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B4
+    PH_MARK(3)
   }
+  PH_FLUSH
   if (pass == 0) {
     // the slab's direct value sums (every wave's adds are in: the last barrier) into sumfix
     const uint32_t* dl = meta + L.dlist();
@@ -695,6 +729,15 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
     meta[L.bcap() + b] = round_up(c, stb ? 4 : 8);
     meta[L.bcnt() + b] = 0u;
   }
+  // A redo lays the direct keys out exactly from 0; past the space planned for them
+  // (H_D16) they overlap level 2's planned regions: then level 2's first pass only
+  // counts (every region emptied: its runs overflow) and its redo lays the regions
+  // out exactly above the direct keys' new end.
+  const uint32_t d16 = hdr[H_D16];
+  if (ov && t16 > d16) {
+    for (uint32_t k = b; k < L.K; k += 1024)
+      if (!((meta[L.dbits() + (k >> 6)] >> ((k >> 1) & 31u)) & 1u)) meta[L.kcap() + k] = 0u;
+  }
   // level-2 items: ITEM2 level-1 records of a super-tile's region (k_rbin2 finds an
   // item's super-tile in istart); the totals are exact either way
   uint32_t all;
@@ -704,6 +747,7 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
   if (b == 0) {
     meta[L.istart() + FS] = all;
     hdr[H_ITEMS] = all;
+    if (ov && t16 > d16) hdr[H_D16] = t16;
     hdr[H_OV2] = 0u;
     hdr[H_REDO2] = 0u;
     hdr[H_REDO1] = ov;
@@ -1051,6 +1095,12 @@ __global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__
 }
 
 }  // namespace
+
+#ifdef L5DH_PHASES
+extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases1(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase1), sizeof(g_phase1), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_fetch_host(const uint32_t* hs, const uint32_t* hv, uint32_t* ds, uint32_t* dv, size_t n,
                              hipStream_t st) {

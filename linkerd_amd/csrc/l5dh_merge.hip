@@ -77,9 +77,11 @@ __global__ __launch_bounds__(256) void k_mpack(const uint32_t* __restrict__ src,
 
 // One wave per series of the slice: the LDS row accumulates every source's entries
 // (a source's words are parsed 64 at a time; escape headers are rare, resolved by a
-// loop over their ballot), then the dense row, the total and the summary.
-constexpr int MDEC_WAVES = 4;
-__global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeSources src, uint32_t nrows,
+// loop over their ballot), then the dense row, the total and the summary.  The
+// sources' word counts and offsets of the row come with one load per lane, the
+// first chunks of MDEC_BATCH sources with loads in flight together.
+constexpr int MDEC_WAVES = 4, MDEC_BATCH = 8;
+__global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint32_t nrows,
                                                              const int64_t* __restrict__ totals, Tables tb,
                                                              int32_t* __restrict__ out_rows,
                                                              Summary88* __restrict__ out_summ) {
@@ -90,14 +92,16 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeSources src, u
   if (r >= nrows) return;  // (wave-uniform; no barriers below)
   uint32_t* row = lrow[w];
   for (int b = lane; b < ROW; b += 64) row[b] = 0u;
-  for (int s = 0; s < src.n; ++s) {
-    const uint32_t* enc = src.enc[s] + src.offs[s][r];
-    const uint32_t nw = src.words[s][r];
+  const uint32_t* __restrict__ enc = src.enc;
+  const size_t ix = (size_t)lane * src.per + r;  // lane s: source s's row r
+  const uint32_t nwl = lane < src.n ? src.words[ix] : 0u;
+  const uint64_t offl = lane < src.n ? src.offs[ix] : 0ull;
+  auto parse = [&](uint32_t x, uint32_t nw, uint64_t off) {
     bool carry = false;  // the chunk's first word is the count of the previous chunk's last header
     for (uint32_t base = 0; base < nw; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       const bool valid = i < nw;
-      const uint32_t x = valid ? enc[i] : 0u;
+      if (base) x = valid ? enc[off + i] : 0u;
       unsigned long long hm = __ballot(valid && (x & CMAX) == CMAX);  // escape headers, or counts that look like one
       unsigned long long pay = 0ull;
       if (carry) {
@@ -119,11 +123,24 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeSources src, u
       if (valid && !((pay >> lane) & 1ull)) {
         const uint32_t b = x >> 21;
         uint32_t c = x & CMAX;
-        if (c == CMAX) c = lane == 63 ? enc[i + 1] : nxt;
+        if (c == CMAX) c = lane == 63 ? enc[off + i + 1] : nxt;
         row[b] += c;  // one wave owns the row; a source holds each bucket once
       }
       carry = next_carry;
     }
+  };
+  for (int s0 = 0; s0 < src.n; s0 += MDEC_BATCH) {  // (s0 <= 56: every lane index below is < 64)
+    uint32_t xs[MDEC_BATCH], nws[MDEC_BATCH];
+    uint64_t offs[MDEC_BATCH];
+#pragma unroll
+    for (int k = 0; k < MDEC_BATCH; ++k) {
+      nws[k] = s0 + k < src.n ? (uint32_t)__builtin_amdgcn_readlane((int)nwl, s0 + k) : 0u;
+      offs[k] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)offl, s0 + k) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(offl >> 32), s0 + k) << 32);
+      xs[k] = (uint32_t)lane < nws[k] ? enc[offs[k] + lane] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < MDEC_BATCH; ++k) parse(xs[k], nws[k], offs[k]);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const SrcLds32 lds{row};
@@ -286,9 +303,10 @@ hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, 
   return exclusive_scan_u32_u64(words, nrows, offs, tmp, st);
 }
 
-hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
+hipError_t merge_decode(const MergeRecv& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
                         Summary88* out_summ, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
+  if (src.n < 1 || src.n > MERGE_MAX_RANKS || nrows > src.per) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_mdecode, dim3((nrows + MDEC_WAVES - 1) / MDEC_WAVES), dim3(64 * MDEC_WAVES), 0, st, src, nrows,
                      totals, tb, out_rows, out_summ);
   return hipGetLastError();

@@ -7,11 +7,12 @@ namespace l5dh {
 
 constexpr int MERGE_MAX_RANKS = 64;
 
-struct MergeSources {  // the encodings of this rank's row slice, one per source rank
-  const uint32_t* enc[MERGE_MAX_RANKS];    // entries
-  const uint32_t* words[MERGE_MAX_RANKS];  // [nrows] words per row
-  const uint64_t* offs[MERGE_MAX_RANKS];   // [nrows] exclusive offsets of the rows' words
-  int n;
+struct MergeRecv {  // the encodings of this rank's row slice from every source rank, source by source
+  const uint32_t* enc;    // entries: source 0's rows, then source 1's, ...
+  const uint32_t* words;  // [n][per] words per row
+  const uint64_t* offs;   // [n][per] exclusive offsets of the rows' words in enc (one scan of words)
+  uint32_t per;           // rows per source slice
+  int n;                  // sources (<= MERGE_MAX_RANKS)
 };
 
 // words[r] = entry words of row r (words needs nrows + 1 slots; rows == nullptr: already
@@ -29,8 +30,8 @@ hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, 
 // dst[i] = sum over k < n of srcs[k][i] (the loopback transport's reductions; dst may be srcs[0])
 hipError_t merge_loop_sum_i32(const int32_t* const* srcs, int n, int32_t* dst, size_t count, hipStream_t st);
 hipError_t merge_loop_sum_i64(const int64_t* const* srcs, int n, int64_t* dst, size_t count, hipStream_t st);
-// summed rows of the slice (out_rows nullable: [nrows][1798]) and their summaries
-hipError_t merge_decode(const MergeSources& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
+// summed rows of the slice (nrows <= src.per; out_rows nullable: [nrows][1798]) and their summaries
+hipError_t merge_decode(const MergeRecv& src, uint32_t nrows, const int64_t* totals, Tables tb, int32_t* out_rows,
                         Summary88* out_summ, hipStream_t st);
 
 }  // namespace l5dh

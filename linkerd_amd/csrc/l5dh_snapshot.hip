@@ -351,7 +351,6 @@ __device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t 
 // per series emits the dense row and the summary (the series' exact sum is its
 // sumfix: the value sums were folded at ingest).  The midpoints are staged once;
 // each wave clears its series' LDS rows right after emitting them.
-template <bool ENCODE>  // the fleet merge's sparse export (out.enc: row encodings, no rows or summaries)
 __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                           uint32_t cold_arg, int final_mode, int reset) {
   constexpr int NT = 1024;
@@ -380,8 +379,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   // Every load is unconditional (clamped indices, masked where used), so no wait for
   // it is placed before the emission.
   const bool one = segs.n == 1;
-  constexpr bool encode = ENCODE;
-  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0, eb = 0;
+  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0;
   bool dirty = false;
   int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
@@ -403,9 +401,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
       x1 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n1 ? a1 + 8 * g : a1));
     }
     fraw = st.sumfix[min(t * TILE + (threadIdx.x & (TILE - 1)), st.S - 1)];
-    if (encode) eb = plan.enc_base[t];
   };
-  __shared__ uint32_t rwl[TILE];  // (sparse export) words of the tile's rows
   const uint4* __restrict__ citem = plan.cold_item;
   const uint32_t last = cold_items ? cold_items - 1u : 0u;  // (clamped prefetch indices stay in the list)
   // Items: a workgroup's first two are blockIdx.x and blockIdx.x + G; the rest come from
@@ -421,7 +417,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   uint4 cn = citem[min(item1, last)];  // the next item's entry, in flight
   __syncthreads();
   for (int par = 0; item < cold_items; par ^= 1) {
-    const uint32_t tc = t, ebc = eb;
+    const uint32_t tc = t;
     const bool dc = dirty;
     if (threadIdx.x < TILE) {
       const uint32_t s = tc * TILE + threadIdx.x;
@@ -460,40 +456,7 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
                         s0 + TILE <= st.S && (oi0 & 1u) == 0u;
-    if (encode) {
-      // (a whole-range resetting export) each row's words, then its entries at its
-      // place in the tile's range of the unpacked encoding (rows in order)
-      for (int loc = w; loc < TILE; loc += NT / 64) {
-        const uint32_t s = s0 + loc;
-        uint32_t nw = 0;
-        if (s < st.S)
-          nw = dc ? row_words(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}})
-                  : row_words(SrcLds16{hist + loc * CROW});
-        if (lane == 0) rwl[loc] = nw;
-      }
-      __syncthreads();
-      for (int loc = w; loc < TILE; loc += NT / 64) {
-        const uint32_t s = s0 + loc;
-        if (s < st.S) {
-          uint32_t at = ebc;
-          for (int l = 0; l < loc; ++l) at += rwl[l];
-          if (dc)
-            row_encode(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}},
-                       out.enc, at);
-          else
-            row_encode(SrcLds16{hist + loc * CROW}, out.enc, at);
-          if (lane == 0) {
-            const uint32_t oi = s - out.first;
-            out.roff[oi] = at;
-            out.words[oi] = rwl[loc];
-            if (out.totals) out.totals[oi] = fixl[loc] + (dc ? st.total[s] : 0);
-          }
-        }
-        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);  // this wave's row, cleared for the next item
-        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    for (int loc = w; !encode && loc < TILE; loc += NT / 64) {
+    for (int loc = w; loc < TILE; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
@@ -553,8 +516,31 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
 // k_accum_cold_h: the cold tiles as half-tile items -- 16 series in one u16-packed LDS
 // histogram (57.6 KB), 512-thread workgroups, two per CU, so one workgroup counts
 // while the other emits its rows (k_accum_cold_p keeps one tile in flight per CU).
-// Item i is half i & 1 of cold item i >> 1.  Not for the sparse export.
+// Item i is half i & 1 of cold item i >> 1.  ENCODE: the fleet merge's sparse export
+// (row encodings, no rows or summaries); half 1's rows start past half 0's room in
+// the tile's encoding range (h0 + 16 words for a clean tile: a row's words never
+// exceed its records; ENC_HALF_CAP for a dirty one).
+#ifdef L5DH_PHASES  // development: per-workgroup phase times of k_accum_cold_h
+__device__ unsigned long long g_phase2[1024 * 8];
+#define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
+#define PH_MARK(k)                                 \
+  if (threadIdx.x == 0) {                          \
+    const unsigned long long ph_n = wall_clock64(); \
+    ph_acc[k] += ph_n - ph_t;                      \
+    ph_t = ph_n;                                   \
+  }
+#define PH_FLUSH                                                          \
+  if (threadIdx.x == 0) {                                                 \
+    for (int k = 0; k < 4; ++k) g_phase2[blockIdx.x * 8 + k] += ph_acc[k]; \
+    g_phase2[blockIdx.x * 8 + 7] += 1;                                    \
+  }
+#else
+#define PH_INIT
+#define PH_MARK(k)
+#define PH_FLUSH
+#endif
 constexpr int HSER = 16;
+template <bool ENCODE>
 __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, State st, Tables tb, Outputs out,
                                                          uint32_t cold_arg, int final_mode, int reset) {
   constexpr int NT = 512;
@@ -581,7 +567,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   // the next item's entry is loaded one item ahead; its sumfix and (one pending
   // segment) each thread's first 16-B group during this item's emission
   const bool one = segs.n == 1;
-  uint32_t t = 0, a = 0, nn = 0, hf = 0;
+  uint32_t t = 0, a = 0, nn = 0, hf = 0, eb = 0;
   bool dirty = false;
   int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u);
@@ -599,7 +585,9 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       x0 = *reinterpret_cast<const uint4*>(b16 + (8 * g < nn ? a + 8 * g : a));
     }
     fraw = st.sumfix[min(t * TILE + HSER * half + (threadIdx.x & (HSER - 1)), st.S - 1)];
+    if (ENCODE) eb = plan.enc_base[t];
   };
+  __shared__ uint32_t rwl[HSER];  // (sparse export) words of the item's rows
   const uint4* __restrict__ citem = plan.cold_item;
   const uint32_t last = cold_tiles ? cold_tiles - 1u : 0u;
   // items: blockIdx.x, blockIdx.x + G, then from the counter, asked two items ahead
@@ -611,8 +599,9 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   if (item < nitems) fetch(citem[item >> 1], item & 1u);
   uint4 cn = citem[min(item1 >> 1, last)];
   __syncthreads();
+  PH_INIT
   for (int par = 0; item < nitems; par ^= 1) {
-    const uint32_t tc = t, hc = hf;
+    const uint32_t tc = t, hc = hf, ebc = eb;
     const bool dc = dirty;
     if (threadIdx.x < HSER) {
       const uint32_t s = tc * TILE + HSER * hc + threadIdx.x;
@@ -628,7 +617,11 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint4 cx = x;
         const uint32_t gn = g + NT;
         x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
+#if defined(L5DH_CEXP) && (L5DH_CEXP & 4)  // timing only: no counting
+        if (cx.x == 0xFFFFFFFFu && cx.y == 0x12345u) hist_add(0, 0);
+#else
         count16(cx, min(8u, nn - 8 * g), hist_add);
+#endif
       }
     } else {
       for (int j = 0; j < segs.n; ++j) {
@@ -639,6 +632,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       }
     }
     __syncthreads();  // counts complete; fixl visible
+    PH_MARK(0)
     fetch(cn, item1 & 1u);  // (past the last item: a harmless refetch)
     const uint32_t item2 = s_next[par];
     cn = citem[min(item2 >> 1, last)];
@@ -648,7 +642,48 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + HSER <= out.count &&
                         s0 + HSER <= st.S && (oi0 & 1u) == 0u;
-    for (int loc = w; loc < HSER; loc += NT / 64) {
+    if (ENCODE) {
+      for (int loc = w; loc < HSER; loc += NT / 64) {
+        const uint32_t s = s0 + loc;
+        uint32_t nw = 0;
+        if (s < st.S)
+          nw = dc ? row_words(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}})
+                  : row_words(SrcLds16{hist + loc * CROW});
+        if (lane == 0) rwl[loc] = nw;
+      }
+      uint32_t hb = ebc;  // this half's first word
+      if (hc) {
+        if (dc) {
+          hb += ENC_HALF_CAP;
+        } else {
+          uint32_t h0 = 0;
+          for (int j = 0; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
+          hb += h0 + HSER;
+        }
+      }
+      __syncthreads();  // rwl complete
+      for (int loc = w; loc < HSER; loc += NT / 64) {
+        const uint32_t s = s0 + loc;
+        if (s < st.S) {
+          uint32_t at = hb;
+          for (int l = 0; l < loc; ++l) at += rwl[l];
+          if (dc)
+            row_encode(SrcSum2<SrcLds16, SrcRow32>{SrcLds16{hist + loc * CROW}, SrcRow32{st.counts + (size_t)s * ROW}},
+                       out.enc, at);
+          else
+            row_encode(SrcLds16{hist + loc * CROW}, out.enc, at);
+          if (lane == 0) {
+            const uint32_t oi = s - out.first;
+            out.roff[oi] = at;
+            out.words[oi] = rwl[loc];
+            if (out.totals) out.totals[oi] = fixl[loc] + (dc ? st.total[s] : 0);
+          }
+        }
+        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);  // cleared for the next item
+        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    for (int loc = w; !ENCODE && loc < HSER; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
       if (s < st.S) {
@@ -665,7 +700,11 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
             }
           }
           put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
+#if defined(L5DH_CEXP) && (L5DH_CEXP & 1)  // timing only (tools/mk_var.sh): no summaries
+          if (g[0] == 0xFFFFFFFFu) out.summ[0].count = g[1];
+#else
           wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+#endif
           if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
@@ -678,6 +717,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     }
     if (linear) {
       __syncthreads();  // the summaries have read the rows
+      PH_MARK(1)
       uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
       constexpr int NCH = HSER * NB / 4;
       for (int c = threadIdx.x; c < NCH; c += NT) {
@@ -688,7 +728,11 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint32_t x = *p0, y = *p1;
         *p0 = 0u;
         *p1 = 0u;
+#if defined(L5DH_CEXP) && (L5DH_CEXP & 2)  // timing only: no dense stores
+        if ((x & y) == 0xFFFFFFFFu) o[c] = make_uint4(x, y, x, y);
+#else
         o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+#endif
       }
     }
     if (threadIdx.x == 0) {
@@ -696,9 +740,11 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       s_next[par ^ 1] = asked;
     }
     __syncthreads();
+    PH_MARK(2)
     item = item1;
     item1 = item2;
   }
+  PH_FLUSH
 }
 
 // One-tile series spaces (S <= 32: C1, the head shard of a many-way C3) fold each
@@ -1053,14 +1099,20 @@ int num_cus() {
 
 }  // namespace
 
+#ifdef L5DH_PHASES
+extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases2(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase2), sizeof(g_phase2), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 hipError_t set_snapshot_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)ACC_COLD_LDS);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold_p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)ACC_COLD_LDS);
+  e = hipFuncSetAttribute((const void*)k_accum_cold_h<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)ACC_COLDH_LDS);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_accum_cold_h, hipFuncAttributeMaxDynamicSharedMemorySize,
+  e = hipFuncSetAttribute((const void*)k_accum_cold_h<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)ACC_COLDH_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
@@ -1093,19 +1145,18 @@ hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State st
   // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
   // may be DEV_COUNT (read on the device)
   const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
+  // half-tile items, two 512-thread workgroups per CU
+  const uint32_t g2 = std::min<uint32_t>(cold_items == DEV_COUNT ? 0xFFFFFFFFu : 2u * cold_items, 2u * (uint32_t)num_cus());
   if (out.enc)
-    hipLaunchKernelGGL(k_accum_cold_p<true>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
+    hipLaunchKernelGGL(k_accum_cold_h<true>, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
 #ifndef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel)
-  else if (true) {
-    // half-tile items, two 512-thread workgroups per CU
-    const uint32_t g2 = std::min<uint32_t>(cold_items == DEV_COUNT ? 0xFFFFFFFFu : 2u * cold_items, 2u * (uint32_t)num_cus());
-    hipLaunchKernelGGL(k_accum_cold_h, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out, cold_items,
-                       final_mode, reset);
-  }
+  else if (true)
+    hipLaunchKernelGGL(k_accum_cold_h<false>, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out,
+                       cold_items, final_mode, reset);
 #endif
   else
-    hipLaunchKernelGGL(k_accum_cold_p<false>, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
+    hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
   return hipGetLastError();
 }

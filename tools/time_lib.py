@@ -40,6 +40,9 @@ def main():
         eng.snapshot_into(summ, counts, reset=True)
     eng.set_param(N.PARAM_TIMING, 1)
     eng.kernel_times(reset=True)
+    core = N.load()
+    phases = [getattr(core, f"l5dh_dev_phases{i}", None) for i in (1, 2)]  # (L5DH_PHASES builds)
+    before = [snap_phases(f) for f in phases]
     for k in range(steps):
         eng.ingest(*batches[k % 2])
         eng.snapshot_into(summ, counts, reset=True)
@@ -47,6 +50,26 @@ def main():
     tot = sum(ms for ms, n in kt.values() if n) / steps
     print(f"{os.path.basename(N.LIB_PATH)}: {tot:.4f} ms/step  " +
           "  ".join(f"{k} {ms / steps:.4f}" for k, (ms, n) in kt.items() if n), flush=True)
+    for name, f, b in zip(("level1", "cold"), phases, before):
+        if f is None:
+            continue
+        a = snap_phases(f)
+        d = [[a[w][k] - b[w][k] for k in range(8)] for w in range(1024)]
+        act = [x for x in d if x[7] > 0]
+        if not act:
+            continue
+        # wall_clock64 runs at 100 MHz: ticks * 0.01 us; per launch, averaged over workgroups
+        per = [sum(x[k] for x in act) / sum(x[7] for x in act) * 0.01 for k in range(4)]
+        print(f"  phases {name} ({len(act)} wgs, us per launch per wg): " +
+              " ".join(f"p{k}={v:.1f}" for k, v in enumerate(per)), flush=True)
+
+
+def snap_phases(f):
+    if f is None:
+        return None
+    buf = (ctypes.c_ulonglong * (1024 * 8))()
+    f(buf)
+    return [[buf[w * 8 + k] for k in range(8)] for w in range(1024)]
 
 
 if __name__ == "__main__":
