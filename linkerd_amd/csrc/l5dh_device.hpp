@@ -249,6 +249,7 @@ __device__ __forceinline__ void row_encode(const Src& src, uint32_t* __restrict_
     const int q = lane + 64 * k;
     const uint4 v = q < NB4 ? src.get4(4 * q) : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t w = merge_words4(v);
+    if (__ballot(w != 0u) == 0ull) continue;  // (wave-uniform) an empty stretch of the row: no scan, no stores
     const uint32_t incl = wave_incl_scan32(w);
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
     uint32_t pos = at + incl - w;

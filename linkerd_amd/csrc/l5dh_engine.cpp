@@ -532,7 +532,7 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   a.dlim16 = dlim16;
   a.thr_min = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, n / (8192ull * c->direct_div)), 0xFFFFFFFFull);
   const uint32_t FS = (c->F + 63) / 64;
-  // + the trash bin, below the hot bin's 8 rank replicas (l5dh_ingest.hip REP0)
+  // + the trash bin (and 8 spare bins)
   a.dmax = std::min<uint32_t>(c->direct_max, ((uint32_t)BIN1_BINS - 9 - FS) / 2);
   a.pct = c->region_pct;
   a.vec = vec;
@@ -755,8 +755,8 @@ int merge_encode_step(l5dh_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((r = ensure(c, c->m_enc, (size_t)bnd[W] * 4 + 16))) return r;
   if (c->m_sparse)  // the export's row encodings packed in row order (one contiguous slice per destination)
-    HIPCHK(c, merge_pack(static_cast<const uint32_t*>(c->m_unpacked.p), static_cast<const uint32_t*>(c->m_roff.p),
-                         words, offs, Sp, static_cast<uint32_t*>(c->m_enc.p), c->stream));
+    HIPCHK(c, merge_pack(static_cast<const uint32_t*>(c->m_unpacked.p), static_cast<const uint32_t*>(c->m_roff.p), offs,
+                         (uint32_t)std::min<size_t>(Sp, c->S), static_cast<uint32_t*>(c->m_enc.p), c->stream));
   else
     HIPCHK(c, merge_encode(static_cast<const int32_t*>(c->merge_counts.p), Sp, offs,
                            static_cast<uint32_t*>(c->m_enc.p), c->stream));
@@ -960,32 +960,42 @@ int loop_collectives(l5dh_ctx** cs, int n, int mode) {
   for (int i = 0; i < n; ++i)
     if ((r = merge_encode_step(cs[i]))) return r;
   if ((r = sync_all(cs, n))) return r;
-  for (int i = 0; i < n; ++i)  // all-gather of the size rows
-    for (int j = 0; j < n; ++j)
-      if (j != i)
-        HIPCHK(cs[j], hipMemcpyAsync(static_cast<uint64_t*>(cs[j]->m_sizes.p) + (size_t)i * W,
-                                     static_cast<const uint64_t*>(cs[i]->m_sizes.p) + (size_t)i * W, (size_t)W * 8,
-                                     hipMemcpyDeviceToDevice, cs[j]->stream));
+  {  // all-gather of the size rows: one copy launch per destination
+    for (int j = 0; j < n; ++j) {
+      LoopCopies l{};
+      for (int i = 0; i < n; ++i)
+        if (i != j) {
+          l.src[l.n] = reinterpret_cast<const uint32_t*>(static_cast<const uint64_t*>(cs[i]->m_sizes.p) + (size_t)i * W);
+          l.dst[l.n] = reinterpret_cast<uint32_t*>(static_cast<uint64_t*>(cs[j]->m_sizes.p) + (size_t)i * W);
+          l.words[l.n++] = (uint64_t)W * 2;
+        }
+      HIPCHK(cs[j], merge_loop_copy(l, cs[j]->stream));
+    }
+  }
   for (int i = 0; i < n; ++i)
     if ((r = merge_recv_step(cs[i]))) return r;
   if ((r = sync_all(cs, n))) return r;
-  for (int q = 0; q < W; ++q) {  // destination q receives every other source's slice q
+  for (int q = 0; q < W; ++q) {  // destination q receives every other source's slice q (one copy launch)
     l5dh_ctx* d = cs[q];
     uint64_t rat = 0;
+    LoopCopies l{};
     for (int p = 0; p < W; ++p) {
       l5dh_ctx* sp = cs[p];
       if (p != q) {
         uint64_t at = 0;
         for (int k = 0; k < q; ++k) at += sp->m_to[k];
-        if (sp->m_to[q])
-          HIPCHK(d, hipMemcpyAsync(static_cast<uint32_t*>(d->r_enc.p) + rat, static_cast<const uint32_t*>(sp->m_enc.p) + at,
-                                   sp->m_to[q] * 4, hipMemcpyDeviceToDevice, d->stream));
-        HIPCHK(d, hipMemcpyAsync(static_cast<uint32_t*>(d->r_words.p) + (size_t)p * per,
-                                 static_cast<const uint32_t*>(sp->m_words.p) + (size_t)q * per, (size_t)per * 4,
-                                 hipMemcpyDeviceToDevice, d->stream));
+        if (sp->m_to[q]) {
+          l.src[l.n] = static_cast<const uint32_t*>(sp->m_enc.p) + at;
+          l.dst[l.n] = static_cast<uint32_t*>(d->r_enc.p) + rat;
+          l.words[l.n++] = sp->m_to[q];
+        }
+        l.src[l.n] = static_cast<const uint32_t*>(sp->m_words.p) + (size_t)q * per;
+        l.dst[l.n] = static_cast<uint32_t*>(d->r_words.p) + (size_t)p * per;
+        l.words[l.n++] = per;
       }
       rat += d->m_from[p];
     }
+    HIPCHK(d, merge_loop_copy(l, d->stream));
     std::vector<const int64_t*> tots(W);  // the totals' reduce-scatter: slice q summed over the sources
     for (int p = 0; p < W; ++p) tots[p] = static_cast<const int64_t*>(cs[p]->merge_totals.p) + (size_t)q * per;
     HIPCHK(d, merge_loop_sum_i64(tots.data(), W, static_cast<int64_t*>(d->recv_totals.p), per, d->stream));

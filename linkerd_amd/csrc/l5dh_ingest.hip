@@ -350,17 +350,9 @@ constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 #define L5DH_RBIN1_NT 1024
 #endif
 constexpr int NT1 = L5DH_RBIN1_NT;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
-// The batch's hottest bin (H_HB0) is ranked on 8 replica counters (LDS words REP0 + (lane &
-// 7), past every bin: bins <= REP0 - 1) so its lanes spread over 8 addresses, and its run
-// is staged as the replicas' runs back to back (subb: the replicas' prefix).
-[[maybe_unused]] constexpr uint32_t REP0 = BIN1_BINS - 8;
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
-#ifdef L5DH_DSUM64
-  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 8;
-#else
   return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
-#endif
 }
 
 template <int NT, int CH>
@@ -381,15 +373,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
-#ifdef L5DH_DSUM64
-  unsigned long long* dsum = reinterpret_cast<unsigned long long*>(lut2 + LUT2_N);  // [DSUM_N] u64 sums
-#else
   uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
-#endif
   __shared__ uint32_t nruns;
-#ifdef L5DH_HOTREP
-  __shared__ uint32_t subb[8];  // hot-bin replicas' stage prefix
-#endif
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
@@ -415,6 +400,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t hi = (uint32_t)min((size_t)lo + per, n);
   bool bad = false;
   PH_INIT
+#ifdef L5DH_PF  // development: the next sub-chunk's first L5DH_PF halves loaded during this one's scatter / write-out
+  constexpr int PFG = L5DH_PF * (PH / 4);  // prefetched 16-B groups per array
+  uint4 pfs[PFG], pfv[PFG];
+  auto prefetch = [&](uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < PFG; ++k) {
+      const uint32_t base = c + 4u * ((uint32_t)k * NT + threadIdx.x);
+      pfs[k] = *reinterpret_cast<const uint4*>(series + base);
+      pfv[k] = *reinterpret_cast<const uint4*>(values + base);
+    }
+  };
+  if (vec && lo + (uint32_t)CH <= hi) prefetch(lo);
+#endif
   for (uint32_t c0 = lo; c0 < hi; c0 += CH) {
     for (uint32_t wd = threadIdx.x; wd < CH / 32; wd += NT) heads[wd] = 0u;
     // records are staged in slot order first (the stage is free until the scatter), so
@@ -434,8 +432,21 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
         for (int k = 0; k < PH / 4; ++k) {
           const uint32_t base = cl + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
+#ifdef L5DH_PF
+          uint4 s4, u4;
+          if (h < L5DH_PF) {
+            s4 = pfs[h * (PH / 4) + k];
+            u4 = pfv[h * (PH / 4) + k];
+          } else {
+            s4 = *reinterpret_cast<const uint4*>(series + base);
+            u4 = *reinterpret_cast<const uint4*>(values + base);
+          }
+          const float4 f4 = make_float4(__uint_as_float(u4.x), __uint_as_float(u4.y), __uint_as_float(u4.z),
+                                        __uint_as_float(u4.w));
+#else
           const uint4 s4 = *reinterpret_cast<const uint4*>(series + base);
           const float4 f4 = *reinterpret_cast<const float4*>(values + base);
+#endif
           sv[4 * k] = s4.x; sv[4 * k + 1] = s4.y; sv[4 * k + 2] = s4.z; sv[4 * k + 3] = s4.w;
           fv[4 * k] = f4.x; fv[4 * k + 1] = f4.y; fv[4 * k + 2] = f4.z; fv[4 * k + 3] = f4.w;
         }
@@ -479,6 +490,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
             }
           }
         }
+        // (The LUT read and the value-sum atomic are branches around the direct slots:
+        // an unconditional, branch-free version -- every slot reading the LUT and adding
+        // 0 to a spare sum -- was slower, bin1 3.89 -> 3.96 ms, profiles/r04i_ab.txt.)
         uint2 dv[4], lv[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
@@ -508,16 +522,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
-#ifdef L5DH_HOTREP
-          const uint32_t ci = bn == hb0 ? REP0 + ((uint32_t)lane & 7u) : bn;
-          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + ci, 1u) | (bn << 15) | (((uint32_t)lane & 7u) << 25);
-#else
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
-#endif
 #if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only: no value sums
-#elif defined(L5DH_DSUM64)
-          if (direct && !esc && p != 0u && pass == 0)
-            atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], (unsigned long long)p);
 #elif defined(L5DH_EXP) && (L5DH_EXP & 2)  // timing only: value sums without the wrap check
           if (direct && !esc && p != 0u && pass == 0) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
 #else
@@ -561,29 +567,13 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     }
     __syncthreads();  // B1: counts complete
     PH_MARK(0)
-#ifdef L5DH_HOTREP
-    const bool rep = !hotrank && hb0 < REP0;
-    uint32_t hotc = 0;  // the hot bin's records (its replicas' sum)
-    if (rep) {
-      const uint4 ra = *reinterpret_cast<const uint4*>(cnt + REP0), rb = *reinterpret_cast<const uint4*>(cnt + REP0 + 4);
-      hotc = ra.x + ra.y + ra.z + ra.w + rb.x + rb.y + rb.z + rb.w;
-      if (threadIdx.x == 0) {
-        subb[0] = 0; subb[1] = ra.x; subb[2] = ra.x + ra.y; subb[3] = ra.x + ra.y + ra.z;
-        const uint32_t a4 = ra.x + ra.y + ra.z + ra.w;
-        subb[4] = a4; subb[5] = a4 + rb.x; subb[6] = a4 + rb.x + rb.y; subb[7] = a4 + rb.x + rb.y + rb.z;
-      }
-    }
-    auto bcount = [&](uint32_t b, uint32_t c) { return rep ? (b == hb0 ? hotc : b >= REP0 ? 0u : c) : c; };
-#else
-    auto bcount = [&](uint32_t, uint32_t c) { return c; };
-#endif
     // run reservations: thread t -> bins t, t + NT, ... (the trash bin TB gets none)
     constexpr int RB = (BIN1_BINS + NT - 1) / NT;
     uint32_t rn[RB], rold[RB], rbase[RB], rcapv[RB];
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
-      rn[j] = rb_bin <= TB ? bcount(rb_bin, cnt[rb_bin]) : 0u;  // records of the bin in this sub-chunk
+      rn[j] = rb_bin <= TB ? cnt[rb_bin] : 0u;  // records of the bin in this sub-chunk
       rold[j] = rbase[j] = rcapv[j] = 0;
       if (rb_bin < TB && rn[j]) {
         rold[j] = atomicAdd(&bcnt[rb_bin], rn[j]);
@@ -591,6 +581,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         rcapv[j] = bcap[rb_bin];
       }
     }
+#ifdef L5DH_PF  // (after the run reservations: their returns do not wait behind these loads)
+    if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
+#endif
     if (wv == 0) {  // one wave: stage offsets and run ranks (DPP scans of 16 bins per lane), run heads
       uint32_t c[16];
 #pragma unroll
@@ -601,7 +594,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t tl = 0, tr = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        c[q] = bcount(16u * lane + q, c[q]);
         tl += c[q];
         tr += c[q] ? 1u : 0u;
       }
@@ -628,12 +620,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = (pk[k] >> 15) & 1023u;
-#ifdef L5DH_HOTREP
-      const uint32_t sb = rep && bin == hb0 ? subb[pk[k] >> 25] : 0u;
-#else
-      const uint32_t sb = 0u;
-#endif
-      stage[(offr[bin] & 0xFFFFu) + sb + (pk[k] & 0x7FFFu)] = rec[k];
+      stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
     }
     if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
       const uint32_t at = threadIdx.x * 64u;
@@ -972,11 +959,11 @@ __global__ __launch_bounds__(NT, 1) void k_rbin2(uint32_t S, uint32_t F, Tables 
         const uint32_t sl = (r[k] >> 21) & 31u, tl = r[k] >> 26;
         const bool valid = 4u * ((uint32_t)(k >> 2) * NT + threadIdx.x) + (uint32_t)(k & 3) < ctot;
         kr[k] = valid ? ((sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16)) : NOKEY;
+        // (branches around the atomics: the branch-free form -- an invalid slot adding 0 to
+        // a count, every slot adding to a sum -- was slower, 0.96 -> 1.03 ms, r04j_ab.txt)
         rank[k] = valid ? atomicAdd(&cnt[kr[k] >> 16], 1u) : 0u;
 #if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only (tools/mk_var.sh): no value sums
         (void)tl;
-#elif defined(L5DH_EXP) && (L5DH_EXP & 8)  // timing only: u32 value sums
-        if (pass == 0 && valid && !esc && p) atomicAdd(reinterpret_cast<uint32_t*>(lsum) + tl * 32u + sl, p);
 #else
         if (pass == 0 && valid && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
 #endif

@@ -36,6 +36,8 @@ constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow bel
 // bucket midpoints (cold tiles), 16 u32 rows (big half-tiles)
 constexpr size_t ACC_COLD_LDS = (size_t)TILE * CROW * 4 + TILE * 8 + ROW * 4;
 constexpr size_t ACC_COLDH_LDS = (size_t)16 * CROW * 4 + 16 * 8 + ROW * 4;  // half-tile cold items
+constexpr int ENC_LIST = 256;  // (sparse export) first-touched buckets listed per row of a half-tile item
+constexpr size_t ACC_COLDHE_LDS = ACC_COLDH_LDS + 2 * 16 * 4 + (size_t)16 * ENC_LIST * 2;
 constexpr size_t ACC_SPLIT_LDS = (size_t)16 * HROW * 4;
 // k_fold1 (samples, not records): u32 rows of 16 series or u16-packed rows of 32, lane-private
 // u64 value sums, the bucket LUT
@@ -58,11 +60,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 // records: [kbase[k], kbase[k] + kcnt[k]) of rec16 -- written by level 1 when tile
 // t is a direct tile of the batch (regions [0, H_D16)), by level 2 otherwise.
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
-#ifdef L5DH_DSUM64  // (development A/B: u64 LDS value sums of the direct series, half as many direct tiles)
-constexpr int DIRECT_MAX = 127;
-#else
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
-#endif
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
 constexpr uint32_t ITEM2 = 16384;   // level-1 records per level-2 item
 struct MetaLayout {

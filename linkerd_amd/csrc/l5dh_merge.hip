@@ -62,17 +62,35 @@ __global__ __launch_bounds__(256) void k_menc(const int32_t* __restrict__ rows, 
 }
 
 // The sparse export's rows (encoded at their tiles' places by the accumulate kernels)
-// packed in row order: one wave per row.
+// packed in row order.  The 16 rows of a half-tile are contiguous in the unpacked
+// encoding (each accumulate path writes a half's rows back to back from the half's
+// first word) and in the packed one, so a wave copies one half-tile as ONE range:
+// roff of its first row, offs of its first and past-last rows (loads unrolled 4 deep).
 __global__ __launch_bounds__(256) void k_mpack(const uint32_t* __restrict__ src, const uint32_t* __restrict__ roff,
-                                               const uint32_t* __restrict__ words, const uint64_t* __restrict__ offs,
-                                               uint32_t nrows, uint32_t* __restrict__ enc) {
-  const uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= nrows) return;
-  const uint32_t n = words[r];
+                                               const uint64_t* __restrict__ offs, uint32_t nrows,
+                                               uint32_t* __restrict__ enc) {
+  const uint32_t r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16u;
+  if (r >= nrows) return;  // (wave-uniform)
+  const uint32_t e = min(r + 16u, nrows);
+  const uint64_t o0 = offs[r];
+  const uint32_t n = (uint32_t)(offs[e] - o0);
   if (n == 0) return;
-  const uint32_t* a = src + roff[r];
-  uint32_t* o = enc + offs[r];
-  for (uint32_t i = lane_id(); i < n; i += 64) o[i] = a[i];
+  const uint32_t* __restrict__ a = src + roff[r];
+  uint32_t* __restrict__ o = enc + o0;
+  const uint32_t lane = (uint32_t)lane_id();
+  for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+    uint32_t x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i = i0 + 64u * q + lane;
+      x[q] = i < n ? a[i] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i = i0 + 64u * q + lane;
+      if (i < n) o[i] = x[q];
+    }
+  }
 }
 
 // One wave per series of the slice: the LDS row accumulates every source's entries
@@ -91,7 +109,7 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
   const uint32_t r = blockIdx.x * MDEC_WAVES + w;
   if (r >= nrows) return;  // (wave-uniform; no barriers below)
   uint32_t* row = lrow[w];
-  for (int b = lane; b < ROW; b += 64) row[b] = 0u;
+  for (int b = lane; b < ROW / 4; b += 64) reinterpret_cast<uint4*>(row)[b] = make_uint4(0u, 0u, 0u, 0u);
   const uint32_t* __restrict__ enc = src.enc;
   const size_t ix = (size_t)lane * src.per + r;  // lane s: source s's row r
   const uint32_t nwl = lane < src.n ? src.words[ix] : 0u;
@@ -124,7 +142,7 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
         const uint32_t b = x >> 21;
         uint32_t c = x & CMAX;
         if (c == CMAX) c = lane == 63 ? enc[off + i + 1] : nxt;
-        row[b] += c;  // one wave owns the row; a source holds each bucket once
+        atomicAdd(&row[b], c);  // (an LDS add: no read-modify-write latency; a source holds each bucket once)
       }
       carry = next_carry;
     }
@@ -145,7 +163,11 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const SrcLds32 lds{row};
   uint32_t g[9];
-  if (out_rows) {
+  // a workgroup whose MDEC_WAVES rows are all in the slice stores them as ONE contiguous
+  // 16-B-aligned range (rows r0.. with r0 even), after the summaries; else row by row
+  const uint32_t r0 = blockIdx.x * MDEC_WAVES;
+  const bool linear = out_rows != nullptr && r0 + MDEC_WAVES <= nrows;  // (then every wave is here)
+  if (out_rows && !linear) {
     int32_t* orow = out_rows + (size_t)r * NB;
     for (int q = lane; q < NB4; q += 64) store4_1798(orow, 4 * q, lds.get4(4 * q));
   }
@@ -153,6 +175,18 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
 #pragma unroll
   for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
   wave_summary(g, lds, totals ? totals[r] : 0, tb.mid, out_summ ? out_summ + r : nullptr);
+  if (linear) {
+    __syncthreads();  // every row complete
+    uint4* o = reinterpret_cast<uint4*>(out_rows + (size_t)r0 * NB);
+    constexpr int NCH = MDEC_WAVES * NB / 4;
+    for (int c = threadIdx.x; c < NCH; c += 64 * MDEC_WAVES) {
+      const int e0 = 4 * c;
+      const int rr = e0 / NB, b0 = e0 - rr * NB;  // (b0 even; a chunk at b0 = 1796 straddles into the next row)
+      const uint2 x = *reinterpret_cast<const uint2*>(&lrow[rr][b0]);
+      const uint2 y = *reinterpret_cast<const uint2*>(b0 == NB - 2 ? &lrow[rr + 1][0] : &lrow[rr][b0 + 2]);
+      o[c] = make_uint4(x.x, x.y, y.x, y.y);
+    }
+  }
 }
 
 // Exclusive u64 prefix of n u32 counts in tiles of SCAN_TILE: k_scan_sums writes
@@ -262,7 +296,40 @@ hipError_t loop_sum(const T* const* srcs, int n, T* dst, size_t count, hipStream
   return hipGetLastError();
 }
 
+// The loopback transport's copies, one launch for many: entry blockIdx.y of the list,
+// its words strided over blockIdx.x.
+__global__ __launch_bounds__(256) void k_loop_copy(LoopCopies l) {
+  const int e = blockIdx.y;
+  if (e >= l.n) return;
+  const uint32_t* __restrict__ src = l.src[e];
+  uint32_t* __restrict__ dst = l.dst[e];
+  const uint64_t n = l.words[e];
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 2048u; i0 < n; i0 += (uint64_t)gridDim.x * 2048u) {
+    uint32_t x[8];  // 8 loads in flight per thread
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t i = i0 + 256u * q + threadIdx.x;
+      x[q] = i < n ? src[i] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t i = i0 + 256u * q + threadIdx.x;
+      if (i < n) dst[i] = x[q];
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t merge_loop_copy(const LoopCopies& l, hipStream_t st) {
+  if (l.n == 0) return hipSuccess;
+  if (l.n < 0 || l.n > LOOP_COPIES_MAX) return hipErrorInvalidValue;
+  uint64_t most = 0;
+  for (int e = 0; e < l.n; ++e) most = std::max<uint64_t>(most, l.words[e]);
+  const uint32_t gx = (uint32_t)std::min<uint64_t>((most + 2047) / 2048, 256);
+  hipLaunchKernelGGL(k_loop_copy, dim3(std::max(gx, 1u), (unsigned)l.n), dim3(256), 0, st, l);
+  return hipGetLastError();
+}
 
 hipError_t merge_loop_sum_i32(const int32_t* const* srcs, int n, int32_t* dst, size_t count, hipStream_t st) {
   return loop_sum(srcs, n, dst, count, st);
@@ -290,10 +357,11 @@ hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* off
   return hipGetLastError();
 }
 
-hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint32_t* words, const uint64_t* offs,
-                      uint32_t nrows, uint32_t* enc, hipStream_t st) {
+hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint64_t* offs, uint32_t nrows, uint32_t* enc,
+                      hipStream_t st) {
   if (nrows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_mpack, dim3((nrows + 3) / 4), dim3(256), 0, st, src, roff, words, offs, nrows, enc);
+  const uint32_t halves = (nrows + 15) / 16;
+  hipLaunchKernelGGL(k_mpack, dim3((halves + 3) / 4), dim3(256), 0, st, src, roff, offs, nrows, enc);
   return hipGetLastError();
 }
 

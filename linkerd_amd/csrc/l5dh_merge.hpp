@@ -21,12 +21,22 @@ struct MergeRecv {  // the encodings of this rank's row slice from every source 
 hipError_t merge_count(const int32_t* rows, uint32_t nrows, uint32_t* words, uint64_t* offs, void* tmp,
                        size_t* tmp_bytes, hipStream_t st);
 hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* offs, uint32_t* enc, hipStream_t st);
-// the sparse export's row encodings (row r: words[r] words at src + roff[r]) packed at offs[r]
-hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint32_t* words, const uint64_t* offs,
-                      uint32_t nrows, uint32_t* enc, hipStream_t st);
+// the sparse export's row encodings (row r at src + roff[r]; the 16 rows of a half-tile back
+// to back) packed at offs[r] (offs[nrows] = the total)
+hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint64_t* offs, uint32_t nrows, uint32_t* enc,
+                      hipStream_t st);
 // offs[0..nrows) = exclusive prefix of words (a received slice); tmp from merge_count's query
 hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
                          hipStream_t st);
+// The loopback transport's copies (device to device, same device), one launch.
+constexpr int LOOP_COPIES_MAX = 128;
+struct LoopCopies {
+  const uint32_t* src[LOOP_COPIES_MAX];
+  uint32_t* dst[LOOP_COPIES_MAX];
+  uint64_t words[LOOP_COPIES_MAX];
+  int n;
+};
+hipError_t merge_loop_copy(const LoopCopies& l, hipStream_t st);
 // dst[i] = sum over k < n of srcs[k][i] (the loopback transport's reductions; dst may be srcs[0])
 hipError_t merge_loop_sum_i32(const int32_t* const* srcs, int n, int32_t* dst, size_t count, hipStream_t st);
 hipError_t merge_loop_sum_i64(const int64_t* const* srcs, int n, int64_t* dst, size_t count, hipStream_t st);

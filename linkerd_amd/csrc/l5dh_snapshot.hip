@@ -559,10 +559,25 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   auto hist_add = [&](uint32_t loc, uint32_t b) {
     atomicAdd(&hist[(loc & (HSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
   };
+  // (sparse export) per row, the buckets in the order they were first touched: the
+  // returning add tells a first touch; tcnt[par][row] counts them (= the row's words:
+  // a cold row's counts stay below the escape), the first ENC_LIST are listed
+  uint32_t* tcnt = reinterpret_cast<uint32_t*>(midl + ROW);      // [2][HSER] (double-buffered by item parity)
+  uint16_t* tlist = reinterpret_cast<uint16_t*>(tcnt + 2 * HSER);  // [HSER][ENC_LIST]
+  int par = 0;
+  auto hist_add_enc = [&](uint32_t loc, uint32_t b) {
+    const uint32_t l = loc & (HSER - 1);
+    const uint32_t old = atomicAdd(&hist[l * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+    if ((((b & 1u) ? old >> 16 : old) & 0xFFFFu) == 0u) {
+      const uint32_t k = atomicAdd(&tcnt[par * HSER + l], 1u);
+      if (k < (uint32_t)ENC_LIST) tlist[l * ENC_LIST + k] = (uint16_t)b;
+    }
+  };
   {
     uint4* p = reinterpret_cast<uint4*>(smem);
     for (int i = threadIdx.x; i < HSER * CROW / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
     for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
+    if (ENCODE && threadIdx.x < 2 * HSER) tcnt[threadIdx.x] = 0u;
   }
   // the next item's entry is loaded one item ahead; its sumfix and (one pending
   // segment) each thread's first 16-B group during this item's emission
@@ -600,7 +615,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   uint4 cn = citem[min(item1 >> 1, last)];
   __syncthreads();
   PH_INIT
-  for (int par = 0; item < nitems; par ^= 1) {
+  for (; item < nitems; par ^= 1) {
     const uint32_t tc = t, hc = hf, ebc = eb;
     const bool dc = dirty;
     if (threadIdx.x < HSER) {
@@ -620,7 +635,10 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
 #if defined(L5DH_CEXP) && (L5DH_CEXP & 4)  // timing only: no counting
         if (cx.x == 0xFFFFFFFFu && cx.y == 0x12345u) hist_add(0, 0);
 #else
-        count16(cx, min(8u, nn - 8 * g), hist_add);
+        if (ENCODE && !dc)
+          count16(cx, min(8u, nn - 8 * g), hist_add_enc);
+        else
+          count16(cx, min(8u, nn - 8 * g), hist_add);
 #endif
       }
     } else {
@@ -628,11 +646,17 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const KeyRange r = seg_key(segs, j, F, tc, hc);
         const uint32_t n = r.e - r.a, g0 = (n + 7) / 8;
         const uint4* p = reinterpret_cast<const uint4*>(r.r16 + r.a);
-        for (uint32_t g = threadIdx.x; g < g0; g += NT) count16(p[g], min(8u, n - 8 * g), hist_add);
+        for (uint32_t g = threadIdx.x; g < g0; g += NT) {
+          if (ENCODE && !dc)
+            count16(p[g], min(8u, n - 8 * g), hist_add_enc);
+          else
+            count16(p[g], min(8u, n - 8 * g), hist_add);
+        }
       }
     }
     __syncthreads();  // counts complete; fixl visible
     PH_MARK(0)
+    if (ENCODE && threadIdx.x < HSER) tcnt[(par ^ 1) * HSER + threadIdx.x] = 0u;  // the next item's (counted after the end barrier)
     fetch(cn, item1 & 1u);  // (past the last item: a harmless refetch)
     const uint32_t item2 = s_next[par];
     cn = citem[min(item2 >> 1, last)];
@@ -642,7 +666,51 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + HSER <= out.count &&
                         s0 + HSER <= st.S && (oi0 & 1u) == 0u;
-    if (ENCODE) {
+    if (ENCODE && !dc) {
+      // a clean item: each row's words = its first touches; entries in touch order (the
+      // decoder adds a source's entries in any order) with the counts from the bins;
+      // only the touched bins are cleared.  A row with more than ENC_LIST touches is
+      // encoded and cleared from its whole bin row.
+      const uint32_t* tc16 = tcnt + par * HSER;
+      uint32_t hb = ebc;
+      if (hc) {
+        uint32_t h0 = 0;
+        for (int j = 0; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
+        hb += h0 + HSER;
+      }
+      PH_MARK(3)
+      for (int loc = w; loc < HSER; loc += NT / 64) {
+        const uint32_t s = s0 + loc;
+        const uint32_t n = tc16[loc];
+        uint32_t at = hb;
+        for (int l = 0; l < loc; ++l) at += tc16[l];
+        uint32_t* row = hist + loc * CROW;
+        if (s < st.S) {
+          if (n <= (uint32_t)ENC_LIST) {
+            for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
+              const uint32_t b = tlist[loc * ENC_LIST + i];
+              const uint32_t c = (row[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
+              out.enc[at + i] = (b << 21) | c;
+            }
+          } else {
+            row_encode(SrcLds16{row}, out.enc, at);
+          }
+          if (lane == 0) {
+            const uint32_t oi = s - out.first;
+            out.roff[oi] = at;
+            out.words[oi] = n;
+            if (out.totals) out.totals[oi] = fixl[loc];
+          }
+        }
+        if (n <= (uint32_t)ENC_LIST) {  // (a wave's LDS ops stay in order: the reads above come first)
+          for (uint32_t i = (uint32_t)lane; i < n; i += 64) row[tlist[loc * ENC_LIST + i] >> 1] = 0u;
+        } else {
+          uint4* hr = reinterpret_cast<uint4*>(row);
+          for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+      }
+      PH_MARK(1)
+    } else if (ENCODE) {
       for (int loc = w; loc < HSER; loc += NT / 64) {
         const uint32_t s = s0 + loc;
         uint32_t nw = 0;
@@ -1113,7 +1181,7 @@ hipError_t set_snapshot_attributes() {
                           (int)ACC_COLDH_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_cold_h<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)ACC_COLDH_LDS);
+                          (int)ACC_COLDHE_LDS);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)k_accum_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_SPLIT_LDS);
   if (e != hipSuccess) return e;
@@ -1148,7 +1216,7 @@ hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State st
   // half-tile items, two 512-thread workgroups per CU
   const uint32_t g2 = std::min<uint32_t>(cold_items == DEV_COUNT ? 0xFFFFFFFFu : 2u * cold_items, 2u * (uint32_t)num_cus());
   if (out.enc)
-    hipLaunchKernelGGL(k_accum_cold_h<true>, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out,
+    hipLaunchKernelGGL(k_accum_cold_h<true>, dim3(g2), dim3(512), ACC_COLDHE_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
 #ifndef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel)
   else if (true)

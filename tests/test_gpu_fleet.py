@@ -95,7 +95,8 @@ def test_loopback_multirank_merge(oracle, W, mode):
     slices of the sparse encoding, the size all-gather, the payload exchange, the
     local slice decoded in place, the totals' reduce-scatter -- or the dense
     all-reduce -- with S not divisible by W, an escaped count (> 2^21 - 1 samples of
-    one bucket on one rank) and two merge intervals through the same buffers, the
+    one bucket on one rank), a cold row with more non-empty buckets than the export's
+    per-row list (ENC_LIST) and two merge intervals through the same buffers, the
     second with kept state (dirty tiles) under new records."""
     from linkerd_amd.engine import HistogramEngine
     S = 4001
@@ -121,6 +122,10 @@ def test_loopback_multirank_merge(oracle, W, mode):
                 heavy = (np.full(2_100_000, 17, np.uint32), np.full(2_100_000, 3.0, np.float32))
                 engines[-1].ingest(*heavy)
                 parts.append(heavy)
+                # series 40 (a cold tile): more non-empty buckets than the export lists per row
+                wide = (np.full(20_000, 40, np.uint32), np.arange(1, 20_001, dtype=np.float32))
+                engines[0].ingest(*wide)
+                parts.append(wide)
             o = _oracle_of(oracle, S, parts)
             want_c, want_t, want_s = o.counts(), o.totals(), o.snapshot()
             res = HistogramEngine.merge_all(engines, mode, with_counts=True)
