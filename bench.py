@@ -66,7 +66,10 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # measured single-GPU steps; the plan is derived from per-tile loads
 # (fleet.plan_shards) -- here the workload's expected load, in a fleet the previous
 # interval's l5dh_tile_totals
-C3_COST = dict(per_sample=5.5e-9, per_series=2.0e-6, per_sample_fold=3.0e-9, fixed=0.05)
+# fleet.CostModel fitted by tools/fit_cost.py to the two round-4 8-way shard sweeps + the C3/C2/C1
+# lines (profiles/r04_shard_sweeps_joint_fit.txt: 19 lines, every one within 4.2 %)
+C3_COST = dict(per_sample=4.05e-9, per_series=1.36e-6, per_sample_fold=2.59e-9, fixed=0.242, per_sample_l2=2.47e-9,
+               per_sample_hot=7.37e-11, fixed_fold=0.0513)
 
 
 def parse():

@@ -54,24 +54,67 @@ def shard_ranges(total_series: int, world: int, weights: Optional[np.ndarray] = 
     return [Shard(r, bounds[r], bounds[r + 1] - bounds[r]) for r in range(world)]
 
 
+def tile_features(tile_loads, direct_max: int = 255, cold_limit: int = 65535) -> Tuple[float, float, float]:
+    """(samples, samples outside the direct tiles, samples in big tiles) of one
+    engine's batch with this per-tile load.  The direct tiles are chosen as k_rplan1
+    does (l5dh_ingest.hip): among the tiles with >= n / 8192 records, those at or
+    above the smallest power of two that keeps <= direct_max of them; their samples
+    skip level 2.  A big tile holds > cold_limit records (accumulated by
+    k_accum_split instead of the cold kernel)."""
+    e = np.asarray(tile_loads, dtype=np.float64)
+    n = float(e.sum())
+    if e.size == 0 or n <= 0:
+        return 0.0, 0.0, 0.0
+    thr_min = max(1.0, float(int(n) // 8192))
+    cand = e[e >= thr_min]
+    direct = np.zeros(e.size, dtype=bool)
+    if direct_max > 0 and cand.size:
+        lg = np.floor(np.log2(np.maximum(cand, 1.0))).astype(np.int64)
+        cnt = np.bincount(lg, minlength=64)
+        kbest, cum = 64, 0
+        for k in range(63, -1, -1):
+            cum += int(cnt[k])
+            if cum > direct_max:
+                break
+            kbest = k
+        if kbest < 64:
+            direct = e >= max(thr_min, 2.0 ** kbest)
+    return n, float(e[~direct].sum()), float(e[e > cold_limit].sum())
+
+
 @dataclass(frozen=True)
 class CostModel:
     """Modelled device time (ms) of one snapshot interval of a series range on one
-    MI355X: `per_sample` for a sample partitioned at ingest and accumulated at the
-    snapshot, `per_series` for a series' dense row + summary (7.2 KB written), and
+    MI355X: `per_sample` for a sample partitioned at ingest (level 1) and accumulated
+    at the snapshot, `per_sample_l2` more for one outside the batch's direct tiles
+    (level 2), `per_sample_hot` more for one in a big tile (> 65535 records: the split
+    accumulate), `per_series` for a series' dense row + summary (7.2 KB written), and
     `per_sample_fold` for a range of at most one tile (32 series), which is folded
-    into its state rows at ingest (k_fold1); `fixed` = launches and plans.  One model
-    for any series count and sample count (bench.py fits it to measured C3 / C2 / C1
-    steps)."""
+    into its state rows at ingest (k_fold1); `fixed` (`fixed_fold` for a folded
+    range) = launches and plans.  One model for any series count and load
+    (tools/fit_cost.py fits it to a measured shard sweep and the C3 / C2 / C1 steps)."""
     per_sample: float
     per_series: float
     per_sample_fold: float
     fixed: float
+    per_sample_l2: float = 0.0
+    per_sample_hot: float = 0.0
+    fixed_fold: Optional[float] = None  # (a folded range's launches; None: `fixed`)
 
-    def range_ms(self, samples: float, series: int) -> float:
+    @property
+    def tiled(self) -> bool:
+        """Whether the model needs a range's per-tile load (not only its totals)."""
+        return bool(self.per_sample_l2 or self.per_sample_hot)
+
+    def range_ms(self, samples: float, series: int, tile_loads=None) -> float:
         if series <= 32:
-            return self.fixed + self.per_sample_fold * samples + self.per_series * series
-        return self.fixed + self.per_sample * samples + self.per_series * series
+            f = self.fixed if self.fixed_fold is None else self.fixed_fold
+            return f + self.per_sample_fold * samples + self.per_series * series
+        t = self.fixed + self.per_sample * samples + self.per_series * series
+        if self.tiled and tile_loads is not None:
+            _, l2, hot = tile_features(tile_loads)
+            t += self.per_sample_l2 * l2 + self.per_sample_hot * hot
+        return t
 
 
 def _per_series(tile_samples, S: int) -> np.ndarray:
@@ -86,25 +129,85 @@ def _per_series(tile_samples, S: int) -> np.ndarray:
     return np.repeat(t / n, n)
 
 
+def _range_tiles(per_series: np.ndarray, first: int, count: int) -> np.ndarray:
+    """The per-tile load of the engine that owns series [first, first + count): its
+    tiles are 32 consecutive series from `first`."""
+    if count <= 0:
+        return np.zeros(0)
+    return np.add.reduceat(per_series[first:first + count], np.arange(0, count, 32))
+
+
+def _shard_ms(x: Shard, per_series: np.ndarray, cost: CostModel) -> float:
+    if not x.count:
+        return 0.0
+    r = per_series[x.first:x.first + x.count]
+    return cost.range_ms(float(r.sum()), x.count, _range_tiles(per_series, x.first, x.count) if cost.tiled else None)
+
+
+def _plan_tiled(per_series: np.ndarray, first: int, S: int, world: int, cost: CostModel) -> List[Shard]:
+    """Contiguous ranges of [first, S) at tile boundaries (multiples of 32 from
+    `first`) minimizing the largest modelled time (bisection on that time; each
+    candidate is checked by filling the ranks greedily, the range cost being
+    monotone in its end)."""
+    T = (S - first + 31) // 32  # tiles
+    ends = [min(first + 32 * k, S) for k in range(T + 1)]
+
+    def ms(t0: int, t1: int) -> float:
+        return _shard_ms(Shard(0, ends[t0], ends[t1] - ends[t0]), per_series, cost) if t1 > t0 else 0.0
+
+    def fill(limit: float) -> Optional[List[int]]:
+        bounds, t = [0], 0
+        for _ in range(world):
+            lo, hi = t, T  # the largest end with ms(t, end) <= limit
+            while lo < hi:
+                mid = (lo + hi + 1) // 2
+                if ms(t, mid) <= limit:
+                    lo = mid
+                else:
+                    hi = mid - 1
+            t = lo
+            bounds.append(t)
+        return bounds if t == T else None
+
+    lo, hi = 0.0, ms(0, T)
+    best = fill(hi)
+    for _ in range(40):
+        if hi - lo <= 1e-4 * hi:
+            break
+        mid = 0.5 * (lo + hi)
+        b = fill(mid)
+        if b is not None:
+            hi, best = mid, b
+        else:
+            lo = mid
+    return [Shard(r, ends[best[r]], ends[best[r + 1]] - ends[best[r]]) for r in range(world)]
+
+
 def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard]:
     """Contiguous series ranges of equal modelled device time, from a per-tile load:
     the records per 32-series tile of the last binned batch (l5dh_tile_totals of the
     rank that held them -- the previous interval's last batch -- or an expected
-    load); a tile's records are spread evenly over its series for the boundaries.  When the first tile alone, folded at ingest, costs less than
+    load); a tile's records are spread evenly over its series for the boundaries.
+    With a tiled model (level-2 and big-tile terms, which depend on a range's own
+    tiles) the ranges split at tile boundaries and minimize the slowest rank's
+    modelled time.  When the first tile alone, folded at ingest, costs less than
     the slowest rank of the plain split, rank 0 takes exactly that tile and the other
     ranks split the rest (a Zipf head concentrates there)."""
     per_series = _per_series(tile_samples, S)
-    w = cost.per_sample * per_series + cost.per_series
-    plain = shard_ranges(S, world, weights=w)
+    if cost.tiled:
+        plain = _plan_tiled(per_series, 0, S, world, cost)
+    else:
+        w = cost.per_sample * per_series + cost.per_series
+        plain = shard_ranges(S, world, weights=w)
     if world == 1 or S <= 32:
         return plain
-
-    def ms(x: Shard) -> float:
-        return cost.range_ms(float(per_series[x.first:x.first + x.count].sum()), x.count) if x.count else 0.0
-
-    rest = shard_ranges(S - 32, world - 1, weights=w[32:])
-    pinned = [Shard(0, 0, 32)] + [Shard(x.rank + 1, x.first + 32, x.count) for x in rest]
-    if max(ms(x) for x in pinned) < max(ms(x) for x in plain):
+    if cost.tiled:
+        rest = _plan_tiled(per_series, 32, S, world - 1, cost)
+        pinned = [Shard(0, 0, 32)] + [Shard(x.rank + 1, x.first, x.count) for x in rest]
+    else:
+        rest = shard_ranges(S - 32, world - 1, weights=w[32:])
+        pinned = [Shard(0, 0, 32)] + [Shard(x.rank + 1, x.first + 32, x.count) for x in rest]
+    if max(_shard_ms(x, per_series, cost) for x in pinned) < max(_shard_ms(x, per_series, cost) for x in plain):
         return pinned
     return plain
 
@@ -112,8 +215,7 @@ def plan_shards(tile_samples, S: int, world: int, cost: CostModel) -> List[Shard
 def plan_ms(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) -> List[float]:
     """Modelled device time (ms) of every rank of a plan."""
     per_series = _per_series(tile_samples, S)
-    return [cost.range_ms(float(per_series[x.first:x.first + x.count].sum()), x.count) if x.count else 0.0
-            for x in shards]
+    return [_shard_ms(x, per_series, cost) for x in shards]
 
 
 def plan_spread(shards: Sequence[Shard], tile_samples, S: int, cost: CostModel) -> float:
