@@ -308,7 +308,7 @@ def result_stream():
     return out
 
 
-def run_c4_loopback(args, result_out):
+def run_c4_loopback(args, result_out, check=True):
     """C4 on one GPU: the W ranks of a sample-sharded fleet as W contexts of this
     device, each ingesting its share of the 1e9 samples, merged by l5dh_merge_all over
     the loopback transport (l5dh_comm_init_loopback: the same encode / size / payload /
@@ -357,9 +357,10 @@ def run_c4_loopback(args, result_out):
         step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    got = sum(int(summ[r][:counts[r], 0].sum()) for r in range(W))
-    assert got == Ntot, f"summary counts sum {got} != {Ntot}"
-    assert sum(int(cnts[r][:counts[r]].sum(dtype=torch.int64)) for r in range(W)) == Ntot
+    if check:  # (tools/phases_c4.py times development builds whose results are not checked)
+        got = sum(int(summ[r][:counts[r], 0].sum()) for r in range(W))
+        assert got == Ntot, f"summary counts sum {got} != {Ntot}"
+        assert sum(int(cnts[r][:counts[r]].sum(dtype=torch.int64)) for r in range(W)) == Ntot
     for e in engines:
         e.set_param(N_.PARAM_TIMING, 1)
         e.kernel_times(reset=True)

@@ -62,7 +62,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
 // Segment metadata (u32 words, `meta`), K = 2 F keys:
 constexpr int DIRECT_MAX = 255;     // direct tiles per batch
 constexpr int BIN1_BINS = 1024;     // level-1 bins: super-tiles (<= 512) + 2 x direct tiles + the trash bin
-constexpr uint32_t ITEM2 = 16384;   // level-1 records per level-2 item
+constexpr uint32_t ITEM2 = 6144;    // level-1 records per level-2 item (two level-2 workgroups per CU)
 struct MetaLayout {
   uint32_t K;
   __host__ __device__ constexpr uint32_t kbase() const { return 0; }

@@ -582,7 +582,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   // the next item's entry is loaded one item ahead; its sumfix and (one pending
   // segment) each thread's first 16-B group during this item's emission
   const bool one = segs.n == 1;
-  uint32_t t = 0, a = 0, nn = 0, hf = 0, eb = 0;
+  uint32_t t = 0, a = 0, nn = 0, hf = 0, eb = 0, h0e = 0;
   bool dirty = false;
   int64_t fraw = 0;
   uint4 x0 = make_uint4(0u, 0u, 0u, 0u);
@@ -595,6 +595,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     dirty = (cx & CI_DIRTY) != 0u;
     a = __builtin_amdgcn_readfirstlane(half ? ci.z : ci.y);
     nn = half ? cw >> 16 : cw & 0xFFFFu;
+    h0e = cw & 0xFFFFu;  // (sparse export) half 0's records in segment 0: the whole count with one segment
     if (one) {
       const uint32_t g = threadIdx.x;
       x0 = *reinterpret_cast<const uint4*>(b16 + (8 * g < nn ? a + 8 * g : a));
@@ -616,18 +617,29 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   __syncthreads();
   PH_INIT
   for (; item < nitems; par ^= 1) {
-    const uint32_t tc = t, hc = hf, ebc = eb;
+    const uint32_t tc = t, hc = hf, ebc = eb, h0c = h0e, ac = a, nc = nn;
     const bool dc = dirty;
+    const uint4 xc = x0;
+    const int64_t fc = fraw;
+    uint32_t item2 = 0, asked = 0;
+    if (ENCODE) {
+      // (sparse items emit little: the next item's entry fields and loads, its successor's
+      // entry and the counter ask go in flight here, ahead of this item's count)
+      item2 = s_next[par];
+      if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);
+      fetch(cn, item1 & 1u);
+      cn = citem[min(item2 >> 1, last)];
+    }
     if (threadIdx.x < HSER) {
       const uint32_t s = tc * TILE + HSER * hc + threadIdx.x;
-      const int64_t f = s < st.S ? fraw : 0;
+      const int64_t f = s < st.S ? fc : 0;
       fixl[threadIdx.x] = f;
       if (f) st.sumfix[s] = 0;
     }
     if (one) {
-      const uint32_t g0 = (nn + 7) / 8;
-      const uint4* p0 = reinterpret_cast<const uint4*>(b16 + a);
-      uint4 x = x0;
+      const uint32_t g0 = (nc + 7) / 8;
+      const uint4* p0 = reinterpret_cast<const uint4*>(b16 + ac);
+      uint4 x = xc;
       for (uint32_t g = threadIdx.x; g < g0; g += NT) {
         const uint4 cx = x;
         const uint32_t gn = g + NT;
@@ -635,10 +647,14 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
 #if defined(L5DH_CEXP) && (L5DH_CEXP & 4)  // timing only: no counting
         if (cx.x == 0xFFFFFFFFu && cx.y == 0x12345u) hist_add(0, 0);
 #else
+#if defined(L5DH_CEXP) && (L5DH_CEXP & 32)  // timing only: the sparse export counts without first-touch lists
+        count16(cx, min(8u, nc - 8 * g), hist_add);
+#else
         if (ENCODE && !dc)
-          count16(cx, min(8u, nn - 8 * g), hist_add_enc);
+          count16(cx, min(8u, nc - 8 * g), hist_add_enc);
         else
-          count16(cx, min(8u, nn - 8 * g), hist_add);
+          count16(cx, min(8u, nc - 8 * g), hist_add);
+#endif
 #endif
       }
     } else {
@@ -657,15 +673,20 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     __syncthreads();  // counts complete; fixl visible
     PH_MARK(0)
     if (ENCODE && threadIdx.x < HSER) tcnt[(par ^ 1) * HSER + threadIdx.x] = 0u;  // the next item's (counted after the end barrier)
-    fetch(cn, item1 & 1u);  // (past the last item: a harmless refetch)
-    const uint32_t item2 = s_next[par];
-    cn = citem[min(item2 >> 1, last)];
-    uint32_t asked = 0;
-    if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);
+    if (!ENCODE) {
+      fetch(cn, item1 & 1u);  // (past the last item: a harmless refetch)
+      item2 = s_next[par];
+      cn = citem[min(item2 >> 1, last)];
+      if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);
+    }
     const uint32_t s0 = tc * TILE + HSER * hc;
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + HSER <= out.count &&
                         s0 + HSER <= st.S && (oi0 & 1u) == 0u;
+#if defined(L5DH_CEXP) && (L5DH_CEXP & 64)  // timing only: no sparse-export emission
+    if (ENCODE) {
+    } else
+#endif
     if (ENCODE && !dc) {
       // a clean item: each row's words = its first touches; entries in touch order (the
       // decoder adds a source's entries in any order) with the counts from the bins;
@@ -674,8 +695,9 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       const uint32_t* tc16 = tcnt + par * HSER;
       uint32_t hb = ebc;
       if (hc) {
-        uint32_t h0 = 0;
-        for (int j = 0; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
+        uint32_t h0 = h0c;
+        if (!one)
+          for (int j = 1; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
         hb += h0 + HSER;
       }
       PH_MARK(3)
@@ -724,8 +746,8 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         if (dc) {
           hb += ENC_HALF_CAP;
         } else {
-          uint32_t h0 = 0;
-          for (int j = 0; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
+          uint32_t h0 = h0c;
+          for (int j = 1; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
           hb += h0 + HSER;
         }
       }

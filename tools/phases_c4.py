@@ -1,5 +1,6 @@
-"""Per-phase device times of the C4 loopback step for an L5DH_PHASES build (tools/mk_var.sh
-<name> -DL5DH_PHASES; L5DH_LIB=linkerd_amd/lib_ab/lib<name>.so).  Development tool (GPU box).
+"""The C4 loopback step of one library build (L5DH_LIB=linkerd_amd/lib_ab/lib<name>.so): step
+time, rank 0's kernel times and -- for an L5DH_PHASES build (tools/mk_var.sh <name>
+-DL5DH_PHASES) -- per-phase device times.  Development tool (GPU box).
   L5DH_LIB=... python tools/phases_c4.py [--loopback 8] [--steps 3]"""
 import ctypes
 import io
@@ -25,12 +26,15 @@ def main():
     from linkerd_amd import _native as N
     core = N.load()
     fns = [getattr(core, f"l5dh_dev_phases{i}", None) for i in (1, 2)]
-    if any(f is None for f in fns):
-        sys.exit("not an L5DH_PHASES build: " + N.LIB_PATH)
     out = io.StringIO()
-    bench.run_c4_loopback(args, out)
-    print(out.getvalue().strip()[:200], flush=True)
+    bench.run_c4_loopback(args, out, check=False)
+    import json
+    d = json.loads(out.getvalue().strip().splitlines()[-1])
+    print(f"{os.path.basename(N.LIB_PATH)}: C4 loopback {d['ms_per_step']} ms/step, per rank {d['config']['per_rank_ms']}: "
+          f"{d['per_rank_kernels_ms'][0]}", flush=True)
     for name, f in zip(("level1", "cold"), fns):
+        if f is None:
+            continue
         d = snap(f)
         act = [x for x in d if x[7] > 0]
         if not act:
