@@ -312,8 +312,9 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // it -- a per-64-entry group prefix (gpre) plus a popcount of the group's bits of
 // the run-head bitmap -- indexing the runs' destination deltas (rdelta[run] = run
 // base - stage offset, or NODEST).  Runs below the first direct bin's rank are u32
-// records (rec32), the others u16 (rec16).  A run that does not fit is dropped and
-// flagged; pass 1 (the redo) exits unless k_rfix1 asked for it and adds nothing to
+// records (rec32), the others u16 (rec16).  The next sub-chunk's first half is loaded
+// after B2, in flight through the scatter and write-out (bin1 3.89 -> 3.65 ms on C3,
+// profiles/r04r_ab.txt, r04s_ab.txt).  A run that does not fit is dropped and flagged; pass 1 (the redo) exits unless k_rfix1 asked for it and adds nothing to
 // sumfix or the error counter.
 //
 // Direct value sums: u32 per direct series in LDS; an add that wraps past 2^32 adds
@@ -400,7 +401,10 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t hi = (uint32_t)min((size_t)lo + per, n);
   bool bad = false;
   PH_INIT
-#ifdef L5DH_PF  // development: the next sub-chunk's first L5DH_PF halves loaded during this one's scatter / write-out
+#ifndef L5DH_PF
+#define L5DH_PF 1
+#endif
+#if L5DH_PF  // the next sub-chunk's first half loaded during this one's scatter / write-out
   constexpr int PFG = L5DH_PF * (PH / 4);  // prefetched 16-B groups per array
   uint4 pfs[PFG], pfv[PFG];
   auto prefetch = [&](uint32_t c) {
@@ -432,7 +436,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
         for (int k = 0; k < PH / 4; ++k) {
           const uint32_t base = cl + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
-#ifdef L5DH_PF
+#if L5DH_PF
           uint4 s4, u4;
           if (h < L5DH_PF) {
             s4 = pfs[h * (PH / 4) + k];
@@ -581,9 +585,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         rcapv[j] = bcap[rb_bin];
       }
     }
-#ifdef L5DH_PF  // (after the run reservations: their returns do not wait behind these loads)
-    if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
-#endif
     if (wv == 0) {  // one wave: stage offsets and run ranks (DPP scans of 16 bins per lane), run heads
       uint32_t c[16];
 #pragma unroll
@@ -617,6 +618,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     }
     __syncthreads();  // B2: offsets, run ranks, heads; every slot-order record read
     PH_MARK(1)
+#if L5DH_PF  // (after B2: the run reservations' returns and the scan never wait behind these loads)
+    if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
+#endif
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
       const uint32_t bin = (pk[k] >> 15) & 1023u;
