@@ -33,6 +33,9 @@ def main():
     S = pl["count"]
     eng = HistogramEngine(S)
     eng.set_stream(stream)
+    for prm, v in ((N.PARAM_DIRECT_MAX, args.direct_max), (N.PARAM_DIRECT_DIV, args.direct_div)):
+        if v is not None:
+            eng.set_param(prm, v)
     summ = torch.empty((S, 11), dtype=torch.int64, device="cuda")
     counts = torch.empty((S, N.NBUCKETS), dtype=torch.int32, device="cuda")
     for k in range(3):
