@@ -220,6 +220,7 @@ struct l5dh_ctx {
   // sparse reduce-scatter (l5dh_merge.hip): this rank's encoding, the received slices
   DevBuf m_words, m_offs, m_enc, m_tmp, m_sizes, r_words, r_offs, r_enc;
   DevBuf m_unpacked, m_roff;  // the sparse export: rows' encodings at their tiles' places, each row's first word
+  size_t m_unpacked_words = 0;  // (the unpacked encoding's size: a bound of the packed one)
   bool m_sparse = false;      // the last export was sparse (reduce-scatter through the collective)
   size_t m_tmp_bytes = 0;
   std::vector<uint64_t> m_to, m_from;  // words to / from every rank
@@ -405,6 +406,7 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode =
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (int r = ensure(c, c->m_unpacked, (size_t)words * 4 + 16)) return r;
+    c->m_unpacked_words = words;
     out.enc = static_cast<uint32_t*>(c->m_unpacked.p);
   }
   // The accumulate kernels are persistent and read their item counts from the plan
@@ -749,24 +751,24 @@ int merge_encode_step(l5dh_ctx* c) {
   uint32_t* words = static_cast<uint32_t*>(c->m_words.p);
   uint64_t* offs = static_cast<uint64_t*>(c->m_offs.p);
   HIPCHK(c, merge_count(nullptr, Sp, words, offs, c->m_tmp.p, &c->m_tmp_bytes, c->stream));  // (words: the export's)
-  std::vector<uint64_t> bnd(W + 1);
-  for (int q = 0; q <= W; ++q)
-    HIPCHK(c, hipMemcpyAsync(&bnd[q], offs + (size_t)q * per, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if ((r = ensure(c, c->m_enc, (size_t)bnd[W] * 4 + 16))) return r;
+  // this rank's row of the size matrix (for the all-gather) written on the device: the
+  // slice sizes reach the host with the matrix, in the receive step's one host wait
+  HIPCHK(c, merge_sizes_row(offs, per, W, static_cast<uint64_t*>(c->m_sizes.p) + (size_t)c->rank * W, c->stream));
+  size_t cap = c->m_unpacked_words;  // the packed encoding is no larger than the unpacked one
+  if (!c->m_sparse) {  // (dense rows encoded: the exact size, one host wait)
+    uint64_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, offs + Sp, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    cap = total;
+  }
+  if ((r = ensure(c, c->m_enc, cap * 4 + 16))) return r;
   if (c->m_sparse)  // the export's row encodings packed in row order (one contiguous slice per destination)
     HIPCHK(c, merge_pack(static_cast<const uint32_t*>(c->m_unpacked.p), static_cast<const uint32_t*>(c->m_roff.p), offs,
                          (uint32_t)std::min<size_t>(Sp, c->S), static_cast<uint32_t*>(c->m_enc.p), c->stream));
   else
     HIPCHK(c, merge_encode(static_cast<const int32_t*>(c->merge_counts.p), Sp, offs,
                            static_cast<uint32_t*>(c->m_enc.p), c->stream));
-  c->m_to.assign(W, 0);
-  for (int q = 0; q < W; ++q) c->m_to[q] = bnd[q + 1] - bnd[q];
   c->m_dense_bytes = (uint64_t)Sp * (NB * 4 + 8);
-  c->m_encoded_bytes = bnd[W] * 4 + (uint64_t)Sp * (4 + 8);  // entries + words per row + totals
-  // this rank's row of the size matrix, for the all-gather
-  HIPCHK(c, hipMemcpyAsync(static_cast<uint64_t*>(c->m_sizes.p) + (size_t)c->rank * W, c->m_to.data(), (size_t)W * 8,
-                           hipMemcpyHostToDevice, c->stream));
   return 0;
 }
 
@@ -784,8 +786,11 @@ int merge_recv_step(l5dh_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(mat.data(), c->m_sizes.p, mat.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->m_from.assign(W, 0);
-  uint64_t all = 0;
+  c->m_to.assign(W, 0);
+  uint64_t all = 0, mine = 0;
   for (int s = 0; s < W; ++s) all += (c->m_from[s] = mat[(size_t)s * W + c->rank]);
+  for (int q = 0; q < W; ++q) mine += (c->m_to[q] = mat[(size_t)c->rank * W + q]);
+  c->m_encoded_bytes = mine * 4 + (uint64_t)per * W * (4 + 8);  // entries + words per row + totals
   int r;
   if ((r = ensure(c, c->r_enc, (size_t)all * 4 + 16)) || (r = ensure(c, c->r_words, (size_t)W * per * 4)) ||
       (r = ensure(c, c->r_offs, (size_t)W * per * 8)) || (r = ensure(c, c->recv_totals, (size_t)per * 8)))

@@ -319,7 +319,19 @@ __global__ __launch_bounds__(256) void k_loop_copy(LoopCopies l) {
   }
 }
 
+// One rank's row of the W x W size matrix: words of each destination's slice.
+__global__ void k_msizes(const uint64_t* __restrict__ offs, uint32_t per, int W, uint64_t* __restrict__ row) {
+  const int q = threadIdx.x;
+  if (q < W) row[q] = offs[(size_t)(q + 1) * per] - offs[(size_t)q * per];
+}
+
 }  // namespace
+
+hipError_t merge_sizes_row(const uint64_t* offs, uint32_t per, int W, uint64_t* row, hipStream_t st) {
+  if (W < 1 || W > MERGE_MAX_RANKS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_msizes, dim3(1), dim3(64), 0, st, offs, per, W, row);
+  return hipGetLastError();
+}
 
 hipError_t merge_loop_copy(const LoopCopies& l, hipStream_t st) {
   if (l.n == 0) return hipSuccess;

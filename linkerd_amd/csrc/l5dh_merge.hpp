@@ -25,6 +25,8 @@ hipError_t merge_encode(const int32_t* rows, uint32_t nrows, const uint64_t* off
 // to back) packed at offs[r] (offs[nrows] = the total)
 hipError_t merge_pack(const uint32_t* src, const uint32_t* roff, const uint64_t* offs, uint32_t nrows, uint32_t* enc,
                       hipStream_t st);
+// row[q] = offs[(q + 1) per] - offs[q per] for q < W (a rank's row of the slice-size matrix)
+hipError_t merge_sizes_row(const uint64_t* offs, uint32_t per, int W, uint64_t* row, hipStream_t st);
 // offs[0..nrows) = exclusive prefix of words (a received slice); tmp from merge_count's query
 hipError_t merge_offsets(const uint32_t* words, uint32_t nrows, uint64_t* offs, void* tmp, size_t tmp_bytes,
                          hipStream_t st);
