@@ -93,12 +93,13 @@ __global__ __launch_bounds__(256) void k_mpack(const uint32_t* __restrict__ src,
   }
 }
 
-// One wave per series of the slice: the LDS row accumulates every source's entries
-// (a source's words are parsed 64 at a time; escape headers are rare, resolved by a
-// loop over their ballot), then the dense row, the total and the summary.  The
-// sources' word counts and offsets of the row come with one load per lane, the
-// first chunks of MDEC_BATCH sources with loads in flight together.
-constexpr int MDEC_WAVES = 4, MDEC_BATCH = 8;
+// A wave per series of the slice at a time: the LDS row accumulates every source's
+// entries (a source's words are parsed 64 at a time; escape headers are rare, resolved
+// by a loop over their ballot), then the dense row, the total and the summary.  The
+// sources' word counts and offsets of a row come with one load per lane (the next
+// row's while this one is decoded), the first chunks of MDEC_BATCH sources with loads
+// in flight together.
+constexpr int MDEC_WAVES = 4, MDEC_BATCH = 8, MDEC_GRID = 1280;  // (5 workgroups per CU: 28.8 KB of LDS each)
 __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint32_t nrows,
                                                              const int64_t* __restrict__ totals, Tables tb,
                                                              int32_t* __restrict__ out_rows,
@@ -106,14 +107,19 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
   __shared__ __attribute__((aligned(16))) uint32_t lrow[MDEC_WAVES][ROW];
   const int w = threadIdx.x >> 6;
   const int lane = lane_id();
-  const uint32_t r = blockIdx.x * MDEC_WAVES + w;
-  if (r >= nrows) return;  // (wave-uniform; no barriers below)
+  // persistent waves: rows r, r + GW, ...; the next row's word counts and offsets are
+  // loaded while this row is decoded (no barriers: a wave owns its LDS row)
+  const uint32_t GW = gridDim.x * MDEC_WAVES;
+  uint32_t r = blockIdx.x * MDEC_WAVES + w;
   uint32_t* row = lrow[w];
   for (int b = lane; b < ROW / 4; b += 64) reinterpret_cast<uint4*>(row)[b] = make_uint4(0u, 0u, 0u, 0u);
   const uint32_t* __restrict__ enc = src.enc;
-  const size_t ix = (size_t)lane * src.per + r;  // lane s: source s's row r
-  const uint32_t nwl = lane < src.n ? src.words[ix] : 0u;
-  const uint64_t offl = lane < src.n ? src.offs[ix] : 0ull;
+  auto meta = [&](uint32_t rr, uint32_t& n, uint64_t& o) {  // lane s: source s's row rr
+    const bool ok = rr < nrows && lane < src.n;
+    const size_t ix = (size_t)lane * src.per + (rr < nrows ? rr : 0u);
+    n = ok ? src.words[ix] : 0u;
+    o = ok ? src.offs[ix] : 0ull;
+  };
   auto parse = [&](uint32_t x, uint32_t nw, uint64_t off) {
     bool carry = false;  // the chunk's first word is the count of the previous chunk's last header
     for (uint32_t base = 0; base < nw; base += 64) {
@@ -147,45 +153,39 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
       carry = next_carry;
     }
   };
-  for (int s0 = 0; s0 < src.n; s0 += MDEC_BATCH) {  // (s0 <= 56: every lane index below is < 64)
-    uint32_t xs[MDEC_BATCH], nws[MDEC_BATCH];
-    uint64_t offs[MDEC_BATCH];
+  uint32_t nwl;
+  uint64_t offl;
+  meta(r, nwl, offl);
+  for (; r < nrows; r += GW) {
+    const uint32_t cnw = nwl;
+    const uint64_t coff = offl;
+    meta(r + GW, nwl, offl);
+    for (int s0 = 0; s0 < src.n; s0 += MDEC_BATCH) {  // (s0 <= 56: every lane index below is < 64)
+      uint32_t xs[MDEC_BATCH], nws[MDEC_BATCH];
+      uint64_t offs[MDEC_BATCH];
 #pragma unroll
-    for (int k = 0; k < MDEC_BATCH; ++k) {
-      nws[k] = s0 + k < src.n ? (uint32_t)__builtin_amdgcn_readlane((int)nwl, s0 + k) : 0u;
-      offs[k] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)offl, s0 + k) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(offl >> 32), s0 + k) << 32);
-      xs[k] = (uint32_t)lane < nws[k] ? enc[offs[k] + lane] : 0u;
+      for (int k = 0; k < MDEC_BATCH; ++k) {
+        nws[k] = s0 + k < src.n ? (uint32_t)__builtin_amdgcn_readlane((int)cnw, s0 + k) : 0u;
+        offs[k] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)coff, s0 + k) |
+                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(coff >> 32), s0 + k) << 32);
+        xs[k] = (uint32_t)lane < nws[k] ? enc[offs[k] + lane] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < MDEC_BATCH; ++k) parse(xs[k], nws[k], offs[k]);
     }
-#pragma unroll
-    for (int k = 0; k < MDEC_BATCH; ++k) parse(xs[k], nws[k], offs[k]);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const SrcLds32 lds{row};
-  uint32_t g[9];
-  // a workgroup whose MDEC_WAVES rows are all in the slice stores them as ONE contiguous
-  // 16-B-aligned range (rows r0.. with r0 even), after the summaries; else row by row
-  const uint32_t r0 = blockIdx.x * MDEC_WAVES;
-  const bool linear = out_rows != nullptr && r0 + MDEC_WAVES <= nrows;  // (then every wave is here)
-  if (out_rows && !linear) {
-    int32_t* orow = out_rows + (size_t)r * NB;
-    for (int q = lane; q < NB4; q += 64) store4_1798(orow, 4 * q, lds.get4(4 * q));
-  }
-  const int ng = lane_groups(lane);
-#pragma unroll
-  for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
-  wave_summary(g, lds, totals ? totals[r] : 0, tb.mid, out_summ ? out_summ + r : nullptr);
-  if (linear) {
-    __syncthreads();  // every row complete
-    uint4* o = reinterpret_cast<uint4*>(out_rows + (size_t)r0 * NB);
-    constexpr int NCH = MDEC_WAVES * NB / 4;
-    for (int c = threadIdx.x; c < NCH; c += 64 * MDEC_WAVES) {
-      const int e0 = 4 * c;
-      const int rr = e0 / NB, b0 = e0 - rr * NB;  // (b0 even; a chunk at b0 = 1796 straddles into the next row)
-      const uint2 x = *reinterpret_cast<const uint2*>(&lrow[rr][b0]);
-      const uint2 y = *reinterpret_cast<const uint2*>(b0 == NB - 2 ? &lrow[rr + 1][0] : &lrow[rr][b0 + 2]);
-      o[c] = make_uint4(x.x, x.y, y.x, y.y);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const SrcLds32 lds{row};
+    if (out_rows) {
+      int32_t* orow = out_rows + (size_t)r * NB;
+      for (int q = lane; q < NB4; q += 64) store4_1798(orow, 4 * q, lds.get4(4 * q));
     }
+    uint32_t g[9];
+    const int ng = lane_groups(lane);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) g[q] = q < ng ? sum4(lds.get4(28 * lane + 4 * q)) : 0u;
+    wave_summary(g, lds, totals ? totals[r] : 0, tb.mid, out_summ ? out_summ + r : nullptr);
+    // cleared for the next row (this wave's LDS operations stay in order: the reads come first)
+    for (int b = lane; b < ROW / 4; b += 64) reinterpret_cast<uint4*>(row)[b] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
@@ -387,7 +387,8 @@ hipError_t merge_decode(const MergeRecv& src, uint32_t nrows, const int64_t* tot
                         Summary88* out_summ, hipStream_t st) {
   if (nrows == 0) return hipSuccess;
   if (src.n < 1 || src.n > MERGE_MAX_RANKS || nrows > src.per) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_mdecode, dim3((nrows + MDEC_WAVES - 1) / MDEC_WAVES), dim3(64 * MDEC_WAVES), 0, st, src, nrows,
+  const uint32_t grid = std::min<uint32_t>((nrows + MDEC_WAVES - 1) / MDEC_WAVES, (uint32_t)MDEC_GRID);
+  hipLaunchKernelGGL(k_mdecode, dim3(grid), dim3(64 * MDEC_WAVES), 0, st, src, nrows,
                      totals, tb, out_rows, out_summ);
   return hipGetLastError();
 }
