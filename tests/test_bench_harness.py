@@ -92,3 +92,45 @@ def test_plan_keeps_the_last_partial_tiles_load():
     assert fleet.plan_spread(shards, t, S, zero) == 1.0
     lopsided = [fleet.Shard(0, 0, 32), fleet.Shard(1, 32, S - 32), fleet.Shard(2, S, 0)]
     assert fleet.plan_spread(lopsided, t, S, cost) >= 1.0
+
+
+def test_tile_features_choose_direct_tiles_as_rplan1():
+    """fleet.tile_features restates k_rplan1's direct-tile rule (l5dh_ingest.hip): among
+    the tiles with >= n / 8192 records, those at or above the smallest power of two that
+    keeps <= 255 of them skip level 2; a big tile holds > 65535 records."""
+    import numpy as np
+    from linkerd_amd import fleet
+    e = np.full(300, 2.0 ** 20)  # one power-of-two bucket holding > 255 tiles: none is direct
+    n, l2, hot = fleet.tile_features(e)
+    assert l2 == n == hot
+    e = np.concatenate([np.full(10, 2.0 ** 21), np.full(300, 2.0 ** 16)])
+    n, l2, hot = fleet.tile_features(e)
+    assert l2 == 300 * 2.0 ** 16 and hot == n
+    e = np.full(50, 60_000.0)  # few cold tiles: all direct, none big
+    assert fleet.tile_features(e)[1:] == (0.0, 0.0)
+    e = np.concatenate([np.full(5, 1e6), np.full(100, 10.0)])  # tiles below n / 8192 are never direct
+    assert fleet.tile_features(e)[1] == 1000.0
+
+
+def test_tiled_plan_minimizes_the_slowest_rank():
+    """With the tiled model the plan's boundaries sit at tile boundaries and no single
+    boundary moved by one tile lowers the slowest rank's modelled time."""
+    sys.path.insert(0, REPO)
+    import bench
+    from linkerd_amd import fleet, synth
+    S, N, world = 60_000, 50_000_000, 4
+    cost = fleet.CostModel(**bench.C3_COST)
+    assert cost.tiled
+    load = bench.expected_tile_load(synth.zipf_cdf(S), N)
+    sh = fleet.plan_shards(load, S, world, cost)
+    assert sum(x.count for x in sh) == S
+    worst = max(fleet.plan_ms(sh, load, S, cost))
+    bounds = [x.first for x in sh] + [S]
+    for r in range(1, world):
+        for d in (-32, 32):
+            b = list(bounds)
+            b[r] += d
+            if not (b[r - 1] <= b[r] <= b[r + 1]):
+                continue
+            alt = [fleet.Shard(k, b[k], b[k + 1] - b[k]) for k in range(world)]
+            assert max(fleet.plan_ms(alt, load, S, cost)) >= worst * (1 - 1e-3)
