@@ -334,8 +334,10 @@ CMAX = 0x1FFFFF  # count field of an entry; CMAX marks a count in the next word
 
 def sparse_encode(rows: np.ndarray):
     """Rows int32 [n][1798] -> (entries u32, words per row u32): per row its non-empty
-    buckets in bucket order, bucket << 21 | count, or bucket << 21 | CMAX followed by
-    the count's 32 bits when count >= CMAX (the encoding k_menc writes)."""
+    buckets, bucket << 21 | count, or bucket << 21 | CMAX followed by the count's 32 bits
+    when count >= CMAX.  Written here in bucket order (as k_menc writes dense rows); the
+    library's sparse export writes a clean cold row's entries in first-touch order, and
+    the decoder adds a source's entries in any order."""
     rows = np.ascontiguousarray(rows, dtype=np.int32).view(np.uint32)
     r, b = np.nonzero(rows)
     c = rows[r, b]
