@@ -302,7 +302,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 }
 
 // ------------------------------------------------------------------------
-// Level 1, one 768-thread workgroup per CU walking its slab in 24K-slot sub-chunks.
+// Level 1, one 1024-thread workgroup per CU walking its slab in 24K-slot sub-chunks.
 // Bins: the FS super-tiles (u32 records with the value, for level 2), two half-bins
 // per direct tile (final u16 records: the sample is bucketized here, and its value
 // added to an LDS sum of its series), and a trash bin (slots with no valid sample:

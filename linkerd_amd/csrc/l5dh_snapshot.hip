@@ -3,8 +3,9 @@
 //
 //   k_plan_a/b     per tile: records over pending segments, cold/big, work items
 //   k_hot_init     zero the rows big tiles accumulate into
-//   k_accum_cold_p cold tile: 32 series in u16-packed LDS bins, fused summary +
-//                  dense flush (persistent)
+//   k_accum_cold_h cold half-tile: 16 series in u16-packed LDS bins, fused summary +
+//                  dense flush, or the sparse export's encoding (persistent, two
+//                  workgroups per CU)
 //   k_accum_split  big half-tile: (half, chunk) partial in u32 LDS bins, flushed
 //                  with global atomics (persistent)
 //   k_hot_finish   summaries of big tiles from their merged rows
@@ -346,6 +347,7 @@ __device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t 
   }
 }
 
+#ifdef L5DH_COLD_TILE  // (development A/B build only)
 // k_accum_cold_p: one 1024-thread workgroup per CU walks the cold tiles (<= 65535
 // records: u16 bins cannot overflow): 32 series in u16-packed LDS bins, then one wave
 // per series emits the dense row and the summary (the series' exact sum is its
@@ -513,9 +515,12 @@ __global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, 
   }
 }
 
+#endif  // L5DH_COLD_TILE
+
 // k_accum_cold_h: the cold tiles as half-tile items -- 16 series in one u16-packed LDS
 // histogram (57.6 KB), 512-thread workgroups, two per CU, so one workgroup counts
-// while the other emits its rows (k_accum_cold_p keeps one tile in flight per CU).
+// while the other emits its rows (the whole-tile k_accum_cold_p, kept only as a
+// -DL5DH_COLD_TILE A/B build, held one tile in flight per CU).
 // Item i is half i & 1 of cold item i >> 1.  ENCODE: the fleet merge's sparse export
 // (row encodings, no rows or summaries); half 1's rows start past half 0's room in
 // the tile's encoding range (h0 + 16 words for a clean tile: a row's words never
@@ -1198,9 +1203,11 @@ extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases2(unsigned 
 #endif
 
 hipError_t set_snapshot_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)ACC_COLD_LDS);
+  hipError_t e = hipSuccess;
+#ifdef L5DH_COLD_TILE
+  e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_COLD_LDS);
   if (e != hipSuccess) return e;
+#endif
   e = hipFuncSetAttribute((const void*)k_accum_cold_h<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)ACC_COLDH_LDS);
   if (e != hipSuccess) return e;
@@ -1234,22 +1241,21 @@ hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
                              int final_mode, int reset, hipStream_t st) {
   if (cold_items == 0) return hipSuccess;
-  // persistent: one 1024-thread workgroup per CU walking the cold tiles; cold_items
-  // may be DEV_COUNT (read on the device)
-  const uint32_t grid = std::min<uint32_t>(cold_items, (uint32_t)num_cus());
-  // half-tile items, two 512-thread workgroups per CU
+  // persistent: half-tile items, two 512-thread workgroups per CU; cold_items may be
+  // DEV_COUNT (read on the device)
   const uint32_t g2 = std::min<uint32_t>(cold_items == DEV_COUNT ? 0xFFFFFFFFu : 2u * cold_items, 2u * (uint32_t)num_cus());
   if (out.enc)
     hipLaunchKernelGGL(k_accum_cold_h<true>, dim3(g2), dim3(512), ACC_COLDHE_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
-#ifndef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel)
-  else if (true)
+#ifdef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel, one 1024-thread workgroup per CU)
+  else
+    hipLaunchKernelGGL(k_accum_cold_p, dim3(std::min<uint32_t>(cold_items, (uint32_t)num_cus())), dim3(1024),
+                       ACC_COLD_LDS, st, segs, plan, state, tb, out, cold_items, final_mode, reset);
+#else
+  else
     hipLaunchKernelGGL(k_accum_cold_h<false>, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
 #endif
-  else
-    hipLaunchKernelGGL(k_accum_cold_p, dim3(grid), dim3(1024), ACC_COLD_LDS, st, segs, plan, state, tb, out,
-                       cold_items, final_mode, reset);
   return hipGetLastError();
 }
 
