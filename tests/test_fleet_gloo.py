@@ -144,3 +144,29 @@ def test_series_sharded_gloo_matches_single_process(tmp_path):
     h = O.OracleHistograms(S)
     h.ingest(series, vals)
     assert np.load(tmp_path / "summ.npy").tobytes() == h.snapshot().tobytes()
+
+
+def test_sparse_decode_takes_a_rows_entries_in_any_order():
+    """The sparse export writes a clean cold row's entries in first-touch order (not
+    bucket order); the decoder's sum does not depend on the order of a source's entries,
+    an escaped count staying right after its header."""
+    rng = np.random.default_rng(3)
+    rows = np.zeros((5, fleet.NB), np.int32)
+    for r in range(5):
+        b = rng.choice(fleet.NB, size=40, replace=False)
+        rows[r, b] = rng.integers(1, 1000, size=40)
+    rows[2, 17] = fleet.CMAX + 5  # an escaped count: header + count word
+    enc, words = fleet.sparse_encode(rows)
+    offs = np.concatenate([[0], np.cumsum(words.astype(np.int64))])
+    shuffled = enc.copy()
+    for r in range(5):  # permute each row's entries, moving escape pairs as units
+        seg = enc[offs[r]:offs[r + 1]]
+        units, i = [], 0
+        while i < seg.size:
+            n = 2 if (int(seg[i]) & fleet.CMAX) == fleet.CMAX else 1
+            units.append(seg[i:i + n])
+            i += n
+        order = rng.permutation(len(units))
+        shuffled[offs[r]:offs[r + 1]] = np.concatenate([units[k] for k in order])
+    np.testing.assert_array_equal(fleet.sparse_decode([(shuffled, words)], 5), rows)
+    np.testing.assert_array_equal(fleet.sparse_decode([(enc, words), (shuffled, words)], 5), 2 * rows)
