@@ -18,10 +18,11 @@ Workloads (synthetic inputs generated on the GPU):
   c4            fleet merge: the same 1M series, the 1e9 samples sample-sharded
                 over the ranks; each rank ingests its share and calls l5dh_merge
                 (sparse export + RCCL exchange + dense rows and summaries of its
-                slice).  `--loopback W` (or `--shard r/W`) runs the whole W-rank merge on
-                this one GPU: W contexts, each ingesting its share, merged through
-                l5dh_merge_all over the loopback transport (device copies instead of
-                xGMI) -- every rank's work, so the per-rank time is ms_per_step / W.
+                slice).  `--loopback W` runs the whole W-rank merge on this one GPU: W
+                contexts, each ingesting its share, merged through l5dh_merge_all over
+                the loopback transport (device copies instead of xGMI) -- every rank's
+                work; ms_per_step / W is a one-GPU per-rank estimate WITHOUT the
+                interconnect (a modelled xGMI term is reported beside it).
   c2            100k series x 1k samples on one GPU (replicas when N > 1).
   c1            1 series x 1e7 samples (replicas when N > 1).
 --piece P streams the batch from pinned host memory in P-sample l5dh_ingest
@@ -52,6 +53,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one MI355X xGMI link (7 per GPU, a full mesh on an 8-GPU node); C4 loopback model only
 S_C3, N_C3 = 1_000_000, 1_000_000_000
 # algorithmic bytes per launch: 8 B per sample read once, 7192 B of
 # final counts + 88 B of summary written once per series; partition / sort passes,
@@ -60,6 +62,10 @@ KERNEL_ALG_BYTES = {
     "bin1": lambda n, s, fleet: 8 * n,                         # reads (series, value) once
     "accum": lambda n, s, fleet: (7192 if fleet else 7280) * s,  # writes counts (+ summary)
 }
+# the engine's timed phases (l5dh_kernel_time ids) -> the default build's kernels in the PMC
+# summary whose per-launch bytes add up to the phase (the two accumulate kernels run
+# side by side: one launch of each per snapshot)
+PMC_KERNELS = {"bin1": ["rbin1w"], "bin2": ["rbin2"], "accum": ["accum_cold_h", "accum_split"]}
 METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # device cost model of one step on MI355X for the C3 shard plan (fleet.CostModel): one
 # per-sample, per-series and fold cost for any series / sample count, fitted to the
@@ -290,9 +296,8 @@ def load_pmc_traffic(path, pl):
         return {}, "PMC summary is of another workload"
     if pm.get("src_hash") != engine_source_hash():
         return {}, "stale: PMC summary measured other engine sources (re-run tools/profile_pmc.sh)"
-    parts = {"bin1": ["rbin1w"], "bin2": ["rbin2"], "accum": ["accum_cold_p", "accum_split"]}
     ks = pm.get("kernels", {})
-    out = {name: int(sum(ks[p]["hbm_bytes_per_launch"] for p in ps)) for name, ps in parts.items()
+    out = {name: int(sum(ks[p]["hbm_bytes_per_launch"] for p in ps)) for name, ps in PMC_KERNELS.items()
            if all(p in ks and "hbm_bytes_per_launch" in ks[p] for p in ps)}
     return out, f"PMC {os.path.basename(path)} (src {pm['src_hash']})"
 
@@ -374,6 +379,9 @@ def run_c4_loopback(args, result_out, check=True):
         e.set_param(N_.PARAM_TIMING, 0)
     mb = [e.merge_bytes() for e in engines]
     ms = elapsed / args.steps * 1e3
+    # what the device copies stand in for: each rank's slices to the W-1 others over its
+    # own xGMI links in parallel (a full mesh: one link per peer), at XGMI_LINK_GBS each
+    xgmi_ms = max(m["sent"] for m in mb) / max(1, W - 1) / (XGMI_LINK_GBS * 1e9) * 1e3
     balg = 8 * Ntot + 7280 * S
     path_gbs = balg / (ms * 1e-3) / 1e9
     line = {
@@ -384,7 +392,14 @@ def run_c4_loopback(args, result_out, check=True):
                                f"{W} ranks, all {W} ranks on this one GPU (l5dh_comm_init_loopback)",
                    "series_total": S, "samples_per_step": Ntot, "ranks": W,
                    "step": "every rank: ingest + sparse export; exchange (device copies); every slice's dense rows "
-                           "+ summaries", "per_rank_ms": round(ms / W, 4)},
+                           "+ summaries",
+                   "per_rank_ms_loopback": round(ms / W, 4),
+                   "per_rank_ms_note": "ms_per_step / W with the ranks serialized on one GPU and the exchange done "
+                                       "by same-device copies: a one-GPU estimate of a rank's device time that "
+                                       "EXCLUDES the interconnect; modelled_xgmi_ms is a model of that term, not "
+                                       "a measurement",
+                   "modelled_xgmi_ms": round(xgmi_ms, 4),
+                   "modelled_xgmi": f"largest per-rank sent bytes / (W-1) links / {XGMI_LINK_GBS} GB/s per link"},
         "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(path_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_step": balg,
                           "formula": "8 B/sample + 7280 B/series for the fleet, once (SURVEY.md §8d)"},
@@ -402,10 +417,9 @@ def run_c4_loopback(args, result_out, check=True):
 
 def run(args):
     result_out = result_stream()
-    if args.workload == "c4" and (args.loopback or args.shard):
-        if args.shard and not args.loopback:
-            args.loopback = int(args.shard.split("/")[1])
-        args.shard = None
+    if args.workload == "c4" and args.shard:
+        sys.exit("bench.py: --shard is a C3 series shard; for the W-rank C4 fleet on one GPU use --loopback W")
+    if args.workload == "c4" and args.loopback:
         return run_c4_loopback(args, result_out)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -554,7 +568,7 @@ def run(args):
     if fleet:
         first, cnt = state["merged"]
         tot = torch.stack([summ[:cnt, 0].sum(), torch.tensor(0, device=dev)])
-        want = n if args.shard else pl["N_total"]  # (--shard: this rank's samples, merged alone)
+        want = pl["N_total"]
     else:
         tot = torch.stack([counts[:S].sum(dtype=torch.int64), summ[:S, 0].sum()])
         want = n
@@ -604,7 +618,7 @@ def run(args):
                     "pricing": "SURVEY.md §8d: bin1 8 B/sample, accum 7280 B/series (7192 for the c4 export)"}
     # path: B_alg of everything this step processed, over the step time and all GPUs' peak
     rows_summarized = pl["S_total"] if not args.shard else S
-    world_c4 = pl["world"] if fleet else 1  # (--shard r/W: the W-rank merge this rank's share belongs to)
+    world_c4 = pl["world"] if fleet else 1
     balg = 8 * (total_samples if not args.shard else n) + 7280 * rows_summarized
     gpus = 1 if args.shard else world
     path_gbs = balg / (ms_per_step * 1e-3) / 1e9

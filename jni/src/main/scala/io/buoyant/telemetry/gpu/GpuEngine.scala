@@ -35,12 +35,34 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
   private[this] val freeIds = new java.util.ArrayDeque[Integer]
   private[this] var nextId = 0
   private[this] val stagings = new ConcurrentLinkedQueue[Staging]
+  // close(): `closed` is set first (no new operation starts, no thread gets a new
+  // Staging); every call that passes `ctx` to native code runs under the read lock, and
+  // the context is released under the write lock, so no call can use a freed context
+  @volatile private[this] var closed = false
+  private[this] var released = false // guarded by the write lock
+  private[this] val rw = new java.util.concurrent.locks.ReentrantReadWriteLock
   private[this] val local = new ThreadLocal[Staging] {
     override def initialValue(): Staging = {
+      if (closed) throw new IllegalStateException("GpuEngine is closed")
       val s = new Staging
       stagings.add(s)
+      if (closed) { // close() may have freed the stagings it saw before this one was added
+        stagings.remove(s)
+        s.free()
+        throw new IllegalStateException("GpuEngine is closed")
+      }
       s
     }
+  }
+
+  /** A call on `ctx`: fails once close() has begun (`closing`: close's own flushes). */
+  private[this] def onCtx[T](closing: Boolean = false)(body: => T): T = {
+    val r = rw.readLock
+    r.lock()
+    try {
+      if (released || (closed && !closing)) throw new IllegalStateException("GpuEngine is closed")
+      body
+    } finally r.unlock()
   }
 
   private[this] def check(rc: Long, what: String): Unit =
@@ -63,7 +85,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
 
     def add(id: Int, value: Float): Unit = synchronized {
       // a thread adding after (or racing with) close() must not write freed native memory
-      if (closed) throw new IllegalStateException("GpuEngine is closed")
+      if (closed || GpuEngine.this.closed) throw new IllegalStateException("GpuEngine is closed")
       ids(cur).putInt(4 * n, id)
       values(cur).putFloat(4 * n, value)
       n += 1
@@ -73,7 +95,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     /** Everything staged reaches the library; returns once both buffers are free. */
     def flush(): Unit = synchronized { if (!closed) flushLocked(waitAll = true) }
 
-    private[this] def flushLocked(waitAll: Boolean): Unit = {
+    private[this] def flushLocked(waitAll: Boolean, closing: Boolean = false): Unit = onCtx(closing) {
       if (n > 0) {
         val m = n
         n = 0 // cleared first: a batch the library refused is dropped, never re-sent (no double count)
@@ -94,7 +116,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     def free(): Unit = synchronized {
       if (!closed) {
         closed = true // first: a failing flush still leaves the Staging closed
-        try flushLocked(waitAll = true)
+        try flushLocked(waitAll = true, closing = true)
         finally for (b <- ids ++ values) Native.pinFree(b)
       }
     }
@@ -108,13 +130,14 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
 
   def release(id: Int): Unit = {
     flush()
-    check(Native.snapshot(ctx, id, 1, null, null, true), "l5dh_snapshot(reset)")
+    onCtx()(check(Native.snapshot(ctx, id, 1, null, null, true), "l5dh_snapshot(reset)"))
     synchronized { freeIds.push(id) }
   }
 
   def add(id: Int, value: Float): Unit = local.get.add(id, value)
 
   def flush(): Unit = {
+    if (closed) throw new IllegalStateException("GpuEngine is closed")
     val it = stagings.iterator
     while (it.hasNext) it.next.flush()
   }
@@ -145,7 +168,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
   def summary(id: Int): HistogramSummary = {
     flush()
     val b = ByteBuffer.allocateDirect(Native.SUMMARY_BYTES).order(ByteOrder.LITTLE_ENDIAN)
-    check(Native.snapshot(ctx, id, 1, b, null, false), "l5dh_snapshot")
+    onCtx()(check(Native.snapshot(ctx, id, 1, b, null, false), "l5dh_snapshot"))
     decode(b, 0)
   }
 
@@ -153,7 +176,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
   def peek(id: Int): Seq[BucketAndCount] = {
     flush()
     val row = ByteBuffer.allocateDirect(4 * Native.NBUCKETS).order(ByteOrder.LITTLE_ENDIAN)
-    check(Native.snapshot(ctx, id, 1, null, row, false), "l5dh_snapshot(counts)")
+    onCtx()(check(Native.snapshot(ctx, id, 1, null, row, false), "l5dh_snapshot(counts)"))
     buckets(row)
   }
 
@@ -161,7 +184,7 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
   def reset(id: Int): Seq[BucketAndCount] = {
     flush()
     val row = ByteBuffer.allocateDirect(4 * Native.NBUCKETS).order(ByteOrder.LITTLE_ENDIAN)
-    check(Native.snapshot(ctx, id, 1, null, row, true), "l5dh_snapshot(counts, reset)")
+    onCtx()(check(Native.snapshot(ctx, id, 1, null, row, true), "l5dh_snapshot(counts, reset)"))
     buckets(row)
   }
 
@@ -175,19 +198,39 @@ final class GpuEngine(val capacity: Int, device: Int = 0, batch: Int = 1 << 16) 
     val n = synchronized(nextId)
     if (n > 0) {
       val out = ByteBuffer.allocateDirect(n * Native.SUMMARY_BYTES).order(ByteOrder.LITTLE_ENDIAN)
-      check(Native.snapshot(ctx, 0, n, out, null, true), "l5dh_snapshot(all, reset)")
+      onCtx()(check(Native.snapshot(ctx, 0, n, out, null, true), "l5dh_snapshot(all, reset)"))
       var i = 0
       while (i < n) { f(i, decode(out, i)); i += 1 }
     }
   }
 
+  /**
+   * Flushes and frees every thread's staging (each one even when another fails), then
+   * releases the context once every in-flight call on it has returned; the first
+   * failure is rethrown after that.  Any later call fails with IllegalStateException.
+   */
   def close(): Unit = {
+    closed = true // first: no new call starts and no thread gets a new Staging
+    var first: Throwable = null
+    def keep(t: Throwable): Unit = if (first == null) first = t
+    val it = stagings.iterator
+    while (it.hasNext) {
+      try it.next.free() // flushed, closed, its pinned buffers freed
+      catch { case t: Throwable => keep(t) }
+    }
+    stagings.clear()
+    val w = rw.writeLock
+    w.lock() // every call that passed the closed check has returned
     try {
-      val it = stagings.iterator
-      while (it.hasNext) it.next.free() // every thread's staging: flushed, closed, its pinned buffers freed
-      stagings.clear()
-      check(Native.sync(ctx), "l5dh_sync") // may report a deferred invalid-id -EINVAL (ABI 3)
-    } finally check(Native.close(ctx), "l5dh_close") // the context is released even then
+      if (!released) {
+        try check(Native.sync(ctx), "l5dh_sync") // may report a deferred invalid-id -EINVAL (ABI 3)
+        catch { case t: Throwable => keep(t) }
+        released = true
+        val rc = Native.close(ctx) // (no l5dh_last_error after this: the context is gone)
+        if (rc < 0) keep(new IllegalStateException(s"l5dh_close failed: $rc"))
+      }
+    } finally w.unlock()
+    if (first != null) throw first
   }
 }
 

@@ -182,6 +182,8 @@ struct l5dh_ctx {
   uint8_t* d_tile_flags = nullptr;
   uint32_t* d_header = nullptr;
   uint32_t* d_enc_base = nullptr;  // [F] sparse export: each tile's first word of the unpacked encoding
+  uint32_t* d_enc_h0 = nullptr;    // [F] sparse export: words reserved for half 0 of a big or dirty tile
+  uint32_t* d_enc_dw = nullptr;    // [2F] sparse export: words of each half of a dirty tile's state rows
   uint32_t* h_header = nullptr;      // pinned: [4] ingest error count (written by k_rfix1)
   uint32_t* h_header_dev = nullptr;  // its device-side address
   uint32_t* d_kest = nullptr;   // [2F] sampled ids per (tile, half) key of the batch being binned
@@ -357,8 +359,8 @@ Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c-
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
 Plan plan(l5dh_ctx* c) {
-  return Plan{c->d_tile_tot, c->d_enc_base, c->d_cold_item, static_cast<uint2*>(c->split_item.p), c->d_hot_list,
-              c->d_tile_flags, c->d_header};
+  return Plan{c->d_tile_tot, c->d_enc_base, c->d_enc_h0, c->d_enc_dw, c->d_cold_item,
+              static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags, c->d_header};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -397,6 +399,8 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode =
     return fail(c, -EINVAL, "internal: the sparse export is a whole-range resetting export");
   {
     KTimer kt(c, L5DH_K_SCAN);
+    // (the sparse export: the dirty tiles' state-row words first, for their encoding ranges)
+    if (encode) HIPCHK(c, launch_enc_dirty(state(c), pl, c->stream));
     HIPCHK(c, launch_plan(sv, c->F, final_mode, c->cold_limit, hc, c->d_dirty, direct_out, encode ? 1 : 0, pl,
                           c->stream));
   }
@@ -734,8 +738,10 @@ int merge_export(l5dh_ctx* c, int mode) {
 // itself through RCCL.  Steps: encode (local, one host wait for the slice sizes),
 // sizes (collective: an all-gather of the words-to matrix), receive buffers (local,
 // one host wait), payload (collective).  l5dh_merge_all groups each collective step
-// over its contexts.
-bool merge_skips_collective(const l5dh_ctx* c) { return c->nranks == 1 && !c->rccl_1rank; }
+// over its contexts.  The forcing parameter applies to an RCCL communicator only: a
+// 1-rank loopback group has no transport that could carry the slice to itself (its
+// copies skip p == q), so it always takes the identity.
+bool merge_skips_collective(const l5dh_ctx* c) { return c->nranks == 1 && (!c->rccl_1rank || c->loopback); }
 
 int merge_encode_step(l5dh_ctx* c) {
   const uint32_t per = merge_per(c);
@@ -1111,7 +1117,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_tile_tot, F * 4) &&
             mal((void**)&c->d_cold_item, (F + 1) * 16) && mal((void**)&c->d_hot_list, F * 4) &&
             mal((void**)&c->d_header, plan_header_words((uint32_t)F) * 4) && mal((void**)&c->d_tile_flags, F) &&
-            mal((void**)&c->d_enc_base, F * 4) &&
+            mal((void**)&c->d_enc_base, F * 4) && mal((void**)&c->d_enc_h0, F * 4) &&
+            mal((void**)&c->d_enc_dw, 2 * F * 4) &&
             mal((void**)&c->d_kest, 2 * F * 4) && mal((void**)&c->d_kprev, 2 * F * 4);
   const size_t meta_bytes = (size_t)meta_layout((uint32_t)F).words() * 4;
   for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].meta, meta_bytes);
@@ -1158,7 +1165,8 @@ int l5dh_close(l5dh_ctx* c) {
   for (auto e : c->ev_pool) hipEventDestroy(e);
   void* ptrs[] = {c->d_lim_pad, c->d_mid,      c->d_base,     c->d_lut,       c->d_lut2,     c->d_counts,
                   c->d_total,   c->d_sumfix,   c->d_dirty,    c->d_err,       c->d_tile_tot, c->d_cold_item,
-                  c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev, c->d_enc_base};
+                  c->d_hot_list, c->d_header,  c->d_tile_flags, c->d_kest,    c->d_kprev, c->d_enc_base,
+                  c->d_enc_h0,  c->d_enc_dw};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& s : c->segs) {

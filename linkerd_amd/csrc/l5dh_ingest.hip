@@ -426,11 +426,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     // only their ranks and bins stay in registers while the sub-chunk is ranked
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
-#if defined(L5DH_EXP) && (L5DH_EXP & 16)  // timing only: every sub-chunk loads the slab's first (L2 hits)
-    const uint32_t cl = lo;
-#else
     const uint32_t cl = c0;
-#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t sv[PH];
@@ -518,28 +514,18 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           const uint32_t di = dv[q].y + (uint32_t)__popc(__builtin_amdgcn_ubfe(dv[q].x, 0, tw));
           const uint32_t p = pl[q];
           uint32_t o;
-#if defined(L5DH_EXP) && (L5DH_EXP & 4)  // timing only: no bucket search
-          const uint32_t bk = p & 2047u;
-          (void)lv;
-#else
           const uint32_t bk = lut2_decode(p, lv[q], o);
-#endif
           const bool esc = p >= V_ESC;
           const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
           rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
-#if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only: no value sums
-#elif defined(L5DH_EXP) && (L5DH_EXP & 2)  // timing only: value sums without the wrap check
-          if (direct && !esc && p != 0u && pass == 0) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
-#else
           if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
             const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
             if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
               atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
           }
-#endif
         }
         // slots 4 (kk NT + thread) + q of this group kk, as loaded
         *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4) * NT + threadIdx.x)) =
@@ -663,11 +649,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
-#if defined(L5DH_EXP) && (L5DH_EXP & 32)  // timing only: no write-out stores
-      if (d == 0x12345u) {
-#else
       if (d != NODEST) {
-#endif
         if (run < nst)
           rec32[i + d] = stage[i];
         else
@@ -916,11 +898,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F,
       if (i < total) {
         const uint32_t x = st[i];
         const uint2 o = oc[x >> 16];
-#if defined(L5DH_EXP) && (L5DH_EXP & 4)  // timing only: no run stores
-        if (o.y == 12345u) rec16[o.y + (i - o.x)] = (uint16_t)(x & 0xFFFFu);
-#else
         if (o.y != INVALID) rec16[o.y + (i - o.x)] = (uint16_t)(x & 0xFFFFu);
-#endif
       }
     }
   };
@@ -972,11 +950,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F,
         // (branches around the atomics: the branch-free form -- an invalid slot adding 0 to
         // a count, every slot adding to a sum -- was slower, 0.96 -> 1.03 ms, r04j_ab.txt)
         rank[k] = valid ? atomicAdd(&cnt[kr[k] >> 16], 1u) : 0u;
-#if defined(L5DH_EXP) && (L5DH_EXP & 1)  // timing only (tools/mk_var.sh): no value sums
-        (void)tl;
-#else
         if (pass == 0 && valid && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
-#endif
       }
     }
     __syncthreads();  // B1: counts complete

@@ -32,9 +32,8 @@ constexpr int MAX_SEG = 8;
 constexpr int WG = 1024;            // threads per workgroup of the heavy kernels
 constexpr uint32_t COLD_LIMIT_MAX = 65535u;  // u16 LDS bins cannot overflow below this
 
-// LDS bytes of the accumulate kernels: 32 u16-packed rows + the tile's sumfix + the
-// bucket midpoints (cold tiles), 16 u32 rows (big half-tiles)
-constexpr size_t ACC_COLD_LDS = (size_t)TILE * CROW * 4 + TILE * 8 + ROW * 4;
+// LDS bytes of the accumulate kernels: 16 u16-packed rows + the half-tile's sumfix + the
+// bucket midpoints (cold half-tiles), 16 u32 rows (big half-tiles)
 constexpr size_t ACC_COLDH_LDS = (size_t)16 * CROW * 4 + 16 * 8 + ROW * 4;  // half-tile cold items
 constexpr int ENC_LIST = 256;  // (sparse export) first-touched buckets listed per row of a half-tile item
 constexpr size_t ACC_COLDHE_LDS = ACC_COLDH_LDS + 2 * 16 * 4 + (size_t)16 * ENC_LIST * 2;
@@ -128,6 +127,8 @@ constexpr uint8_t TF_SOLO = 8;     // big tile of a direct_out snapshot, clean, 
 struct Plan {
   uint32_t* tile_tot;      // [F]
   uint32_t* enc_base;      // [F] (sparse export) the tile's first word in the unpacked encoding
+  uint32_t* enc_h0;        // [F] (sparse export) words reserved for half 0 of a big or dirty tile (half 1 follows)
+  uint32_t* enc_dw;        // [2F] (sparse export) words of each half of a dirty tile's state rows (k_enc_dirty)
   uint4* cold_item;        // [F] cold item -> {tile | CI_DIRTY, a0, a1, n0 | n1 << 16}: segment 0's
                            // key ranges (rec16) of the tile's halves
   uint2* split_item;       // [split items] {tile | half << 15, chunk} of big tiles
@@ -139,9 +140,16 @@ struct Plan {
 };
 __host__ __device__ constexpr uint32_t plan_header_words(uint32_t F) { return 6 + 4 * ((F + 1023) / 1024); }
 // Sparse export (the fleet merge's reduce-scatter): words a tile's rows may take in the
-// unpacked encoding -- a clean cold tile at most its records (<= 65535 per tile: no
-// escaped counts), a big or dirty tile two halves of 16 rows x 3596 words at most
+// unpacked encoding (a row: one word per non-empty bucket, a second one per count >=
+// MERGE_CMAX) -- a clean cold tile at most its records (<= 65535 per tile: no escaped
+// counts); a half of a clean big tile min(its records, 16 NB) + records / MERGE_CMAX;
+// a half of a dirty tile its state rows' words (counted by k_enc_dirty) + 2 per record
+// (a record adds at most one non-empty bucket and one escape); never more than
+// ENC_HALF_CAP.  So the unpacked encoding of F <= 2^15 tiles stays below 2^32 words,
+// and near the records (not 2x the dense rows) unless the state rows are dense.
 constexpr uint32_t ENC_HALF_CAP = 16u * 2u * NB + 16u;
+static_assert((uint64_t)((1u << 20) / TILE) * 2u * ENC_HALF_CAP < (1ull << 32),
+              "the unpacked encoding's u32 word offsets (L5DH_MAX_SERIES = 2^20 series)");
 
 struct Outputs {
   Summary88* summ;         // nullable, index = series - first
@@ -191,6 +199,7 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
                         uint32_t* err, bool vec, bool wide, hipStream_t st);
 
 // ---- snapshot launchers (l5dh_snapshot.hip) ----
+hipError_t launch_enc_dirty(State st, Plan plan, hipStream_t st_);
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
                        const uint8_t* dirty, int direct_out, int encode, Plan plan, hipStream_t st);
 // The accumulate launches take UPPER BOUNDS of their item counts (no host round

@@ -60,8 +60,18 @@ __device__ __forceinline__ PlanCls plan_classify(const Segs& segs, uint32_t F, u
   return r;
 }
 
-__device__ __forceinline__ uint32_t enc_cap(const PlanCls& c, uint32_t tot, bool dirty) {
-  return (c.hot || dirty) ? 2u * ENC_HALF_CAP : tot + TILE;
+// (ENC_HALF_CAP's comment) the tile's words; h0w: those reserved for half 0 of a big or
+// dirty tile
+__device__ __forceinline__ uint32_t enc_half(uint32_t recs, bool dirty, uint32_t state_words) {
+  const uint32_t w = dirty ? state_words + 2u * min(recs, 16u * NB) : min(recs, 16u * NB) + recs / MERGE_CMAX;
+  return min(w + 16u, ENC_HALF_CAP);
+}
+__device__ __forceinline__ uint32_t enc_cap(const PlanCls& c, uint32_t tot, bool dirty, const Plan& plan, uint32_t t,
+                                            uint32_t& h0w) {
+  if (!c.hot && !dirty) return tot + TILE;
+  const uint32_t dw0 = dirty ? plan.enc_dw[2 * t] : 0u, dw1 = dirty ? plan.enc_dw[2 * t + 1] : 0u;
+  h0w = enc_half(c.h0, dirty, dw0);
+  return h0w + enc_half(tot - c.h0, dirty, dw1);
 }
 
 __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit,
@@ -73,7 +83,8 @@ __global__ __launch_bounds__(1024) void k_plan_a(Segs segs, uint32_t F, int fina
   if (t < F) {
     uint32_t tot;
     c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
-    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0);
+    uint32_t h0w = 0;
+    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0, plan, t, h0w);
     plan.tile_tot[t] = tot;
   }
   const uint32_t v[4] = {c.ci, c.hot, c.si, c.ec};
@@ -124,14 +135,17 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
   __syncthreads();
   const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
   PlanCls c{0u, 0u, 0u, 0u, 0u};
-  uint32_t tot = 0;
+  uint32_t tot = 0, eh0 = 0;
   if (t < F) {
     c = plan_classify(segs, F, t, tot, final_mode, cold_limit, hot_chunk);
-    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0);
+    if (encode) c.ec = enc_cap(c, tot, dirty[t] != 0, plan, t, eh0);
   }
   uint32_t pv[4] = {c.ci, c.hot, c.si, c.ec}, ptot[4];
   block_excl_scan4<1024>(pv, lds4, ptot);
-  if (encode && t < F) plan.enc_base[t] = base[3] + pv[3];
+  if (encode && t < F) {
+    plan.enc_base[t] = base[3] + pv[3];
+    plan.enc_h0[t] = eh0;
+  }
   const uint32_t ca = base[0] + pv[0];
   const uint32_t xa = base[1] + pv[1];
   uint32_t sa = base[2] + pv[2];
@@ -347,184 +361,15 @@ __device__ __forceinline__ void count_tile(const Segs& sg, uint32_t F, uint32_t 
   }
 }
 
-#ifdef L5DH_COLD_TILE  // (development A/B build only)
-// k_accum_cold_p: one 1024-thread workgroup per CU walks the cold tiles (<= 65535
-// records: u16 bins cannot overflow): 32 series in u16-packed LDS bins, then one wave
-// per series emits the dense row and the summary (the series' exact sum is its
-// sumfix: the value sums were folded at ingest).  The midpoints are staged once;
-// each wave clears its series' LDS rows right after emitting them.
-__global__ __launch_bounds__(1024, 1) void k_accum_cold_p(Segs segs, Plan plan, State st, Tables tb, Outputs out,
-                                                          uint32_t cold_arg, int final_mode, int reset) {
-  constexpr int NT = 1024;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t cold_items = cold_arg != DEV_COUNT ? cold_arg : plan.header[0];
-  uint32_t* hist = smem;                                        // [32][900] u16 pairs
-  int64_t* fixl = reinterpret_cast<int64_t*>(smem + TILE * CROW);  // [32] sumfix of the item's series
-  int32_t* midl = reinterpret_cast<int32_t*>(fixl + TILE);      // [NB] bucket midpoints (the summary's lookups)
-  const int w = threadIdx.x >> 6;
-  const int lane = lane_id();
-  const bool keep = !(final_mode && reset);
-  const uint32_t F = st.F;
-  Tables tbl = tb;
-  tbl.mid = midl;
-  auto hist_add = [&](uint32_t loc, uint32_t b) {
-    atomicAdd(&hist[(loc & 31u) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-  };
-  {
-    uint4* p = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < TILE * CROW / 4; i += NT) p[i] = make_uint4(0, 0, 0, 0);
-    for (int i = threadIdx.x; i < NB; i += NT) midl[i] = tb.mid[i];
-  }
-  // The next item is fetched during this item's emission (its latency hides behind the
-  // dense stores), from its cold-item entry loaded one item earlier: sumfix and -- one
-  // pending segment, the common case -- each thread's first 16-B group of both halves.
-  // Every load is unconditional (clamped indices, masked where used), so no wait for
-  // it is placed before the emission.
-  const bool one = segs.n == 1;
-  uint32_t t = 0, a0 = 0, a1 = 0, n0 = 0, n1 = 0;
-  bool dirty = false;
-  int64_t fraw = 0;
-  uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0;
-  const uint16_t* const b16 = segs.rec16[0];
-  auto fetch = [&](uint4 ci) {
-    // (the entry stays in VGPRs until here, where it becomes scalars: converted at its
-    // load, it would be waited for there)
-    asm volatile("" : "+v"(ci.x), "+v"(ci.y), "+v"(ci.z), "+v"(ci.w));
-    const uint32_t cx = __builtin_amdgcn_readfirstlane(ci.x), cw = __builtin_amdgcn_readfirstlane(ci.w);
-    t = cx & 0x7FFFu;
-    dirty = (cx & CI_DIRTY) != 0u;
-    a0 = __builtin_amdgcn_readfirstlane(ci.y);
-    a1 = __builtin_amdgcn_readfirstlane(ci.z);
-    n0 = cw & 0xFFFFu;
-    n1 = cw >> 16;
-    if (one) {
-      const uint32_t g = threadIdx.x;
-      x0 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n0 ? a0 + 8 * g : a0));
-      x1 = *reinterpret_cast<const uint4*>(b16 + (8 * g < n1 ? a1 + 8 * g : a1));
-    }
-    fraw = st.sumfix[min(t * TILE + (threadIdx.x & (TILE - 1)), st.S - 1)];
-  };
-  const uint4* __restrict__ citem = plan.cold_item;
-  const uint32_t last = cold_items ? cold_items - 1u : 0u;  // (clamped prefetch indices stay in the list)
-  // Items: a workgroup's first two are blockIdx.x and blockIdx.x + G; the rest come from
-  // a counter (2G, 2G + 1, ... in the order workgroups ask), so a workgroup that starts
-  // late -- its CU held by a k_accum_split workgroup -- takes fewer.  Each index is asked
-  // for two items ahead (the entry is loaded one item ahead) and passed through LDS.
-  __shared__ uint32_t s_next[2];
-  uint32_t* const ctr = plan.header + 2;  // zeroed by k_plan_b
-  const uint32_t G2 = 2u * gridDim.x;
-  if (threadIdx.x == 0) s_next[0] = G2 + atomicAdd(ctr, 1u);
-  uint32_t item = blockIdx.x, item1 = blockIdx.x + gridDim.x;
-  if (item < cold_items) fetch(citem[item]);
-  uint4 cn = citem[min(item1, last)];  // the next item's entry, in flight
-  __syncthreads();
-  for (int par = 0; item < cold_items; par ^= 1) {
-    const uint32_t tc = t;
-    const bool dc = dirty;
-    if (threadIdx.x < TILE) {
-      const uint32_t s = tc * TILE + threadIdx.x;
-      const int64_t f = s < st.S ? fraw : 0;
-      fixl[threadIdx.x] = f;
-      if (f) st.sumfix[s] = 0;
-    }
-    if (one) {
-      // group g of both halves: the prefetched first one, then g + NT, ...
-      const uint32_t g0 = (n0 + 7) / 8, g1 = (n1 + 7) / 8, gm = max(g0, g1);
-      const uint4* p0 = reinterpret_cast<const uint4*>(b16 + a0);
-      const uint4* p1 = reinterpret_cast<const uint4*>(b16 + a1);
-      uint4 x = x0, y = x1;
-      for (uint32_t g = threadIdx.x; g < gm; g += NT) {
-        const uint4 cx = x, cy = y;
-        const uint32_t gn = g + NT;
-        x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
-        y = gn < g1 ? p1[gn] : make_uint4(0u, 0u, 0u, 0u);
-        count16(cx, g < g0 ? min(8u, n0 - 8 * g) : 0u, hist_add);
-        count16(cy, g < g1 ? min(8u, n1 - 8 * g) : 0u, hist_add);
-      }
-    } else {
-      count_tile<NT>(segs, F, tc, hist_add);
-    }
-    __syncthreads();  // counts complete; fixl visible
-    fetch(cn);  // (past the last item: a harmless refetch of the last entry)
-    const uint32_t item2 = s_next[par];
-    cn = citem[min(item2, last)];
-    uint32_t asked = 0;
-    if (threadIdx.x == 0) asked = G2 + atomicAdd(ctr, 1u);  // (stored at the end of the emission)
-    const uint32_t s0 = tc * TILE;
-    // linear emission: a clean whole tile inside the output range of a resetting
-    // snapshot (the bench path) has its 32 dense rows stored as ONE contiguous range
-    // of 14384 16-B chunks by the whole workgroup in step -- 5.6 TB/s against 4.1 for
-    // per-wave rows (tools/mb_store.hip) -- after the per-series summaries
-    const uint32_t oi0 = s0 - out.first;
-    const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + TILE <= out.count &&
-                        s0 + TILE <= st.S && (oi0 & 1u) == 0u;
-    for (int loc = w; loc < TILE; loc += NT / 64) {
-      const uint32_t s = s0 + loc;
-      const uint32_t* row = hist + loc * CROW;
-      if (s < st.S) {
-        if (linear) {
-          const int ng = lane_groups(lane);
-          uint32_t g[9], nw = 0;
-#pragma unroll
-          for (int q = 0; q < 9; ++q) {
-            g[q] = 0u;
-            if (q < ng) {
-              const uint4 v = SrcLds16{row}.get4(28 * lane + 4 * q);
-              g[q] = sum4(v);
-              nw += merge_words4(v);
-            }
-          }
-          put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
-          wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
-          if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
-        } else {
-          emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
-        }
-      }
-      if (!linear) {  // this wave owns the row: clear it for the next item (a wave's LDS ops stay in order)
-        uint4* hr = reinterpret_cast<uint4*>(hist + loc * CROW);
-        for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    if (linear) {
-      __syncthreads();  // the summaries have read the rows
-      // the 32 rows' stores as one range (chunk c = flat elements 4c..4c+3 of
-      // [32][1798]: two u16 pairs), each clearing the words it read
-      uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
-      constexpr int NCH = TILE * NB / 4;
-      for (int c = threadIdx.x; c < NCH; c += NT) {
-        const int e0 = 4 * c;
-        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
-        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
-        // the second pair is the next word (one ds_read2), except for the chunk that
-        // straddles into the next row (b0 = 1796; word 899 of a row is never written)
-        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
-        const uint32_t x = *p0, y = *p1;
-        *p0 = 0u;
-        *p1 = 0u;
-        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
-      }
-    }
-    if (threadIdx.x == 0) {
-      st.dirty[tc] = keep ? 1 : 0;
-      s_next[par ^ 1] = asked;
-    }
-    __syncthreads();  // rows cleared, fixl consumed, the next index visible
-    item = item1;
-    item1 = item2;
-  }
-}
-
-#endif  // L5DH_COLD_TILE
 
 // k_accum_cold_h: the cold tiles as half-tile items -- 16 series in one u16-packed LDS
 // histogram (57.6 KB), 512-thread workgroups, two per CU, so one workgroup counts
-// while the other emits its rows (the whole-tile k_accum_cold_p, kept only as a
-// -DL5DH_COLD_TILE A/B build, held one tile in flight per CU).
+// while the other emits its rows (round 4: -0.12 ms of accumulate against one whole
+// tile per 1024-thread workgroup, which held one tile in flight per CU).
 // Item i is half i & 1 of cold item i >> 1.  ENCODE: the fleet merge's sparse export
 // (row encodings, no rows or summaries); half 1's rows start past half 0's room in
 // the tile's encoding range (h0 + 16 words for a clean tile: a row's words never
-// exceed its records; ENC_HALF_CAP for a dirty one).
+// exceed its records; Plan::enc_h0 for a dirty one).
 #ifdef L5DH_PHASES  // development: per-workgroup phase times of k_accum_cold_h
 __device__ unsigned long long g_phase2[1024 * 8];
 #define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
@@ -651,18 +496,10 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint4 cx = x;
         const uint32_t gn = g + NT;
         x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
-#if defined(L5DH_CEXP) && (L5DH_CEXP & 4)  // timing only: no counting
-        if (cx.x == 0xFFFFFFFFu && cx.y == 0x12345u) hist_add(0, 0);
-#else
-#if defined(L5DH_CEXP) && (L5DH_CEXP & 32)  // timing only: the sparse export counts without first-touch lists
-        count16(cx, min(8u, nc - 8 * g), hist_add);
-#else
         if (ENCODE && !dc)
           count16(cx, min(8u, nc - 8 * g), hist_add_enc);
         else
           count16(cx, min(8u, nc - 8 * g), hist_add);
-#endif
-#endif
       }
     } else {
       for (int j = 0; j < segs.n; ++j) {
@@ -690,10 +527,6 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
     const uint32_t oi0 = s0 - out.first;
     const bool linear = !keep && !dc && out.counts != nullptr && s0 >= out.first && oi0 + HSER <= out.count &&
                         s0 + HSER <= st.S && (oi0 & 1u) == 0u;
-#if defined(L5DH_CEXP) && (L5DH_CEXP & 64)  // timing only: no sparse-export emission
-    if (ENCODE) {
-    } else
-#endif
     if (ENCODE && !dc) {
       // a clean item: each row's words = its first touches; entries in touch order (the
       // decoder adds a source's entries in any order) with the counts from the bins;
@@ -751,7 +584,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       uint32_t hb = ebc;  // this half's first word
       if (hc) {
         if (dc) {
-          hb += ENC_HALF_CAP;
+          hb += plan.enc_h0[tc];
         } else {
           uint32_t h0 = h0c;
           for (int j = 1; j < segs.n; ++j) h0 += seg_key_count(segs, j, F, 2 * tc);
@@ -797,11 +630,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
             }
           }
           put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
-#if defined(L5DH_CEXP) && (L5DH_CEXP & 1)  // timing only (tools/mk_var.sh): no summaries
-          if (g[0] == 0xFFFFFFFFu) out.summ[0].count = g[1];
-#else
           wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
-#endif
           if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
@@ -825,11 +654,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint32_t x = *p0, y = *p1;
         *p0 = 0u;
         *p1 = 0u;
-#if defined(L5DH_CEXP) && (L5DH_CEXP & 2)  // timing only: no dense stores
-        if ((x & y) == 0xFFFFFFFFu) o[c] = make_uint4(x, y, x, y);
-#else
         o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
-#endif
       }
     }
     if (threadIdx.x == 0) {
@@ -1090,7 +915,7 @@ __global__ __launch_bounds__(WG) void k_hot_finish(Plan plan, State st, Tables t
       if (lane == 0) rw16[w] = nw;
       __syncthreads();
       if (s < st.S) {
-        uint32_t at = plan.enc_base[t] + half * ENC_HALF_CAP;
+        uint32_t at = plan.enc_base[t] + (half ? plan.enc_h0[t] : 0u);
         for (int l = 0; l < w; ++l) at += rw16[l];
         row_encode(src, out.enc, at);
         if (lane == 0) {
@@ -1204,10 +1029,6 @@ extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases2(unsigned 
 
 hipError_t set_snapshot_attributes() {
   hipError_t e = hipSuccess;
-#ifdef L5DH_COLD_TILE
-  e = hipFuncSetAttribute((const void*)k_accum_cold_p, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ACC_COLD_LDS);
-  if (e != hipSuccess) return e;
-#endif
   e = hipFuncSetAttribute((const void*)k_accum_cold_h<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)ACC_COLDH_LDS);
   if (e != hipSuccess) return e;
@@ -1219,6 +1040,31 @@ hipError_t set_snapshot_attributes() {
   e = hipFuncSetAttribute((const void*)k_fold1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FOLD16_LDS);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)k_fold1<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)FOLD32_LDS);
+}
+
+// Sparse export: the words of each half of a dirty tile's state rows (one wave per
+// row, 8 rows per wave), so k_plan_a/b size the tile's encoding from them instead of
+// the dense worst case (a merge after a non-resetting snapshot made every
+// touched tile dirty, and the encoding twice the dense rows).
+__global__ __launch_bounds__(256) void k_enc_dirty(State st, Plan plan) {
+  __shared__ uint32_t hw[2];
+  const uint32_t t = blockIdx.x;
+  if (!st.dirty[t]) return;  // (workgroup-uniform; clean tiles' words are never read)
+  if (threadIdx.x < 2) hw[threadIdx.x] = 0u;
+  __syncthreads();
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  for (int r = w; r < TILE; r += 4) {
+    const uint32_t s = t * TILE + (uint32_t)r;
+    const uint32_t nw = s < st.S ? row_words(SrcRow32{st.counts + (size_t)s * ROW}) : 0u;
+    if (lane == 0 && nw) atomicAdd(&hw[r >> 4], nw);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) plan.enc_dw[2 * t + threadIdx.x] = hw[threadIdx.x];
+}
+
+hipError_t launch_enc_dirty(State st, Plan plan, hipStream_t s) {
+  hipLaunchKernelGGL(k_enc_dirty, dim3(st.F), dim3(256), 0, s, st, plan);
+  return hipGetLastError();
 }
 
 hipError_t launch_plan(Segs segs, uint32_t F, int final_mode, uint32_t cold_limit, uint32_t hot_chunk,
@@ -1247,15 +1093,9 @@ hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State st
   if (out.enc)
     hipLaunchKernelGGL(k_accum_cold_h<true>, dim3(g2), dim3(512), ACC_COLDHE_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
-#ifdef L5DH_COLD_TILE  // (development A/B: the whole-tile kernel, one 1024-thread workgroup per CU)
-  else
-    hipLaunchKernelGGL(k_accum_cold_p, dim3(std::min<uint32_t>(cold_items, (uint32_t)num_cus())), dim3(1024),
-                       ACC_COLD_LDS, st, segs, plan, state, tb, out, cold_items, final_mode, reset);
-#else
   else
     hipLaunchKernelGGL(k_accum_cold_h<false>, dim3(g2), dim3(512), ACC_COLDH_LDS, st, segs, plan, state, tb, out,
                        cold_items, final_mode, reset);
-#endif
   return hipGetLastError();
 }
 

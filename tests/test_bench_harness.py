@@ -134,3 +134,29 @@ def test_tiled_plan_minimizes_the_slowest_rank():
                 continue
             alt = [fleet.Shard(k, b[k], b[k + 1] - b[k]) for k in range(world)]
             assert max(fleet.plan_ms(alt, load, S, cost)) >= worst * (1 - 1e-3)
+
+
+def test_pmc_kernel_map_matches_the_committed_summary():
+    """Every kernel that bench.load_pmc_traffic sums for a timed phase exists in the
+    committed PMC summary of the default build (profiles/pmc_latest.json), so each
+    priced phase of the bench line carries its measured traffic; the accumulate
+    phase is the sum of its two side-by-side kernels."""
+    sys.path.insert(0, REPO)
+    import bench
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    pm = json.load(open(path))
+    ks = pm["kernels"]
+    for phase, kernels in bench.PMC_KERNELS.items():
+        for k in kernels:
+            assert k in ks and "hbm_bytes_per_launch" in ks[k], f"{phase}: {k} not in {path}"
+    assert set(bench.PMC_KERNELS["accum"]) == {"accum_cold_h", "accum_split"}
+    pl = {"workload": pm["workload"], "count": pm["series"], "samples": pm["samples"]}
+    from linkerd_amd import _native
+    real = _native.engine_source_hash
+    try:
+        _native.engine_source_hash = lambda: pm["src_hash"]  # (the committed summary's sources)
+        out, note = bench.load_pmc_traffic(path, pl)
+    finally:
+        _native.engine_source_hash = real
+    want = int(sum(ks[k]["hbm_bytes_per_launch"] for k in bench.PMC_KERNELS["accum"]))
+    assert out["accum"] == want and set(out) == set(bench.PMC_KERNELS), (out, note)

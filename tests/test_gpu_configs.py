@@ -197,3 +197,111 @@ def test_c4_fleet_merge_8_way_1m_series(oracle):
     _eq(got, o.snapshot(), "C4 sampled")
     del series, values, acc, part, m
     torch.cuda.empty_cache()
+
+
+def test_c4_product_sparse_merge_8_way_1m_series(oracle):
+    """C4 through the PRODUCT merge at full size: 8 loopback ranks (one device), 1M
+    series, the 1e9-sample C3 batch sample-sharded (sample i -> rank i mod 8), merged
+    by l5dh_merge_all(MERGE_REDUCE_SCATTER) -- the sparse export from the accumulate
+    kernels (first-touch lists and whole-row encodes), the half-tile pack, the
+    per-destination slices (~125K rows each), the exchange, the totals' reduce-scatter
+    and the decode + summaries of every slice.  Two intervals through the same
+    buffers (seeds 3, 4).  Every rank's slice is checked against a torch ground truth
+    independent of the engine (bincount of series * 1798 + upper_bound(limits,
+    (long)value), exact int64 sums), its summaries against one engine's snapshot of the
+    whole batch, and a sample of series by a bit-exact oracle replay."""
+    import torch
+    from linkerd_amd.engine import HistogramEngine
+    S, n, W = 1_000_000, 1_000_000_000, 8
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    lib = N.load()
+    series = torch.empty(n, dtype=torch.int32, device=dev)
+    values = torch.empty(n, dtype=torch.float32, device=dev)
+    cdf = torch.from_numpy(synth.zipf_cdf(S)).to(dev)
+    lim = torch.from_numpy(oracle.limits().astype(np.int64)).to(dev)
+    per = -(-S // W)
+    engines = [HistogramEngine(S) for _ in range(W)]
+    summ = [torch.empty((per, 11), dtype=torch.int64, device=dev) for _ in range(W)]
+    rows = [torch.empty((per, N.NBUCKETS), dtype=torch.int32, device=dev) for _ in range(W)]
+    tots = [torch.empty(per, dtype=torch.int64, device=dev) for _ in range(W)]
+    ctxs = (ctypes.c_void_p * W)(*[e._ctx.value for e in engines])
+    o_arr = (ctypes.c_void_p * W)(*[t.data_ptr() for t in summ])
+    c_arr = (ctypes.c_void_p * W)(*[t.data_ptr() for t in rows])
+    t_arr = (ctypes.c_void_p * W)(*[t.data_ptr() for t in tots])
+    firsts, counts = (ctypes.c_uint32 * W)(), (ctypes.c_uint32 * W)()
+    try:
+        HistogramEngine.comm_init_loopback(engines)
+        for seed in (3, 4):
+            assert _synth().l5ds_gen_zipf(ctypes.c_void_p(series.data_ptr()), ctypes.c_void_p(values.data_ptr()),
+                                          ctypes.c_uint64(n), ctypes.c_uint64(S), ctypes.c_void_p(cdf.data_ptr()),
+                                          ctypes.c_uint64(seed), ctypes.c_double(0.8), ctypes.c_uint64(0),
+                                          ctypes.c_uint32(0), ctypes.c_void_p(stream)) == 0
+            torch.cuda.synchronize()
+            # the single-engine summaries of the whole batch (the engine's own dense path)
+            one = HistogramEngine(S)
+            one_summ = torch.empty((S, 11), dtype=torch.int64, device=dev)
+            one.ingest(series, values)
+            one.snapshot_into(one_summ, None, reset=True)
+            torch.cuda.synchronize()
+            one.close()
+            del one
+            torch.cuda.empty_cache()
+            for r, e in enumerate(engines):
+                sr, vr = series[r::W].contiguous(), values[r::W].contiguous()
+                torch.cuda.synchronize()
+                e.ingest(sr, vr)
+                torch.cuda.synchronize()
+                del sr, vr
+            rc = lib.l5dh_merge_all(ctxs, W, N.MERGE_REDUCE_SCATTER, o_arr, c_arr, t_arr, firsts, counts)
+            if rc != 0:
+                engines[0]._check(rc, "l5dh_merge_all")
+            torch.cuda.synchronize()
+            # the torch ground truth, independent of the engine's LUTs and kernels
+            truth = torch.zeros(S * N.NBUCKETS, dtype=torch.int32, device=dev)
+            sums = torch.zeros(S, dtype=torch.int64, device=dev)
+            step = 100_000_000
+            for o in range(0, n, step):
+                ids = series[o:o + step].long()
+                v = values[o:o + step].to(torch.int64)  # values in [0, 1e9]: (long)value
+                b = torch.searchsorted(lim, v, right=True)
+                truth.index_add_(0, ids * N.NBUCKETS + b, torch.ones_like(b, dtype=torch.int32))
+                sums.index_add_(0, ids, v)
+                del ids, v, b
+            truth = truth.view(S, N.NBUCKETS)
+            for r in range(W):
+                f, c = firsts[r], counts[r]
+                assert (f, c) == (min(r * per, S), max(0, min(per, S - r * per))), f"rank {r} slice"
+                bad = (rows[r][:c] != truth[f:f + c]).any(dim=1)
+                assert int(bad.sum()) == 0, \
+                    f"seed {seed} rank {r}: {int(bad.sum())} rows differ, first {(torch.nonzero(bad)[:8].flatten() + f).tolist()}"
+                assert torch.equal(tots[r][:c], sums[f:f + c]), f"seed {seed} rank {r}: totals"
+                assert torch.equal(summ[r][:c], one_summ[f:f + c]), f"seed {seed} rank {r}: summaries vs one engine"
+                assert torch.equal(summ[r][:c, 0], truth[f:f + c].sum(dim=1, dtype=torch.int64))
+                assert torch.equal(summ[r][:c, 3], sums[f:f + c])
+            del truth, sums, one_summ
+            # bit-exact oracle replay of sampled series (head, direct/split, cold; every rank's slice)
+            rng = np.random.default_rng(100 + seed)
+            chosen = np.unique(np.concatenate([[0, 1, 2, 31, 32, 2047, 9000, per - 1, per, 3 * per + 7, S - 1],
+                                               rng.integers(10_000, S, 53)])).astype(np.int64)
+            sel = torch.from_numpy(chosen).to(dev)
+            m = torch.isin(series, sel.to(torch.int32))
+            s_sub = series[m].cpu().numpy().astype(np.int64)
+            v_sub = values[m].cpu().numpy()
+            del m
+            o = oracle.OracleHistograms(chosen.size)
+            o.ingest(np.searchsorted(chosen, s_sub).astype(np.uint32), v_sub, threads=THREADS)
+            want_c, want_s = o.counts(), o.snapshot()
+            for i, sid in enumerate(chosen):
+                r = int(sid) // per
+                k = int(sid) - firsts[r]
+                np.testing.assert_array_equal(rows[r][k].cpu().numpy(), want_c[i], err_msg=f"series {sid} counts")
+                got = summ[r][k].cpu().numpy().view(N.SUMMARY_DTYPE)
+                for fld in N.SUMMARY_FIELDS:
+                    assert got[fld][0] == want_s[fld][i], f"series {sid} field {fld}: {got[fld][0]} vs {want_s[fld][i]}"
+    finally:
+        for e in engines:
+            e.close()
+        del series, values, rows, summ, tots
+        torch.cuda.empty_cache()

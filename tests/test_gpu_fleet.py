@@ -165,3 +165,28 @@ def test_comm_rejects_more_than_64_ranks_before_any_state_is_consumed(oracle):
         assert got.tobytes() == o.snapshot().tobytes()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("forced", [0, 1])
+def test_one_rank_loopback_merge_ignores_the_rccl_forcing_param(oracle, forced):
+    """a 1-rank loopback group has no transport that could send the slice to
+    itself, so L5DH_PARAM_MERGE_RCCL_1RANK must not route it into the exchange (whose
+    decode would read receive buffers nothing wrote): the merge is the identity."""
+    from linkerd_amd.engine import HistogramEngine
+    S = 2500
+    eng = HistogramEngine(S)
+    try:
+        eng.set_param(N.PARAM_MERGE_RCCL_1RANK, forced)
+        HistogramEngine.comm_init_loopback([eng])
+        eng.set_param(N.PARAM_MERGE_RCCL_1RANK, forced)  # either order
+        for rnd in range(2):  # stale buffers of a first merge must not leak into a second
+            s, v = synth.c3(S=S, N=200_000 + 1000 * rnd, seed=83 + rnd)
+            eng.ingest(s, v)
+            o = _oracle_of(oracle, S, [(s, v)])
+            (first, count, summ, cnt, tot), = HistogramEngine.merge_all([eng], N.MERGE_REDUCE_SCATTER, with_counts=True)
+            assert (first, count) == (0, S)
+            np.testing.assert_array_equal(cnt, o.counts())
+            np.testing.assert_array_equal(tot, o.totals())
+            assert summ.tobytes() == o.snapshot().tobytes()
+    finally:
+        eng.close()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build linkerd_amd/lib_ab/lib<name>.so from the working tree with extra compile
-# flags (experiment switches such as -DL5DH_EXP=n).  Development tool.
+# flags (e.g. -DL5DH_PHASES for per-workgroup phase stamps).  Development tool.
 #   tools/mk_var.sh <name> [hipcc flags...]
 set -e
 cd "$(dirname "$0")/../linkerd_amd/csrc"
