@@ -295,7 +295,10 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_REDO2] = 0;
     hdr[H_HB0] = (b1 >> 10) ? (uint32_t)(b1 & 1023u) : NOKEY;
     hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
-    hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
+#ifndef L5DH_HSDIV
+#define L5DH_HSDIV 2
+#endif
+    hdr[H_HS] = all > 0 && (b1 >> 10) * L5DH_HSDIV >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
@@ -367,7 +370,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
                                                   uint32_t* __restrict__ err, int vec, int pass) {
   constexpr int PT = CH / NT;  // slots per thread, loaded and ranked in halves
   constexpr int PH = PT / 2;
-  static_assert(PH % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
+#ifndef L5DH_GS
+#define L5DH_GS 4
+#endif
+  constexpr int GS = L5DH_GS;  // slots whose LDS lookups and atomics are issued together
+  static_assert(PH % 4 == 0 && PH % GS == 0 && GS % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* stage = smem;                                        // [CH] records, sorted by bin
   uint32_t* cnt = stage + CH;                                    // [BIN1_BINS]
@@ -427,6 +434,17 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
     const uint32_t cl = c0;
+#ifdef L5DH_H1EARLY  // the second half's loads issued before the first half is ranked
+    uint4 h1s[PH / 4], h1v[PH / 4];
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < PH / 4; ++k) {
+        const uint32_t base = cl + 4u * ((uint32_t)(PH / 4 + k) * NT + threadIdx.x);
+        h1s[k] = *reinterpret_cast<const uint4*>(series + base);
+        h1v[k] = *reinterpret_cast<const uint4*>(values + base);
+      }
+    }
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t sv[PH];
@@ -440,6 +458,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           if (h < L5DH_PF) {
             s4 = pfs[h * (PH / 4) + k];
             u4 = pfv[h * (PH / 4) + k];
+#ifdef L5DH_H1EARLY
+          } else if (h == 1) {
+            s4 = h1s[k];
+            u4 = h1v[k];
+#endif
           } else {
             s4 = *reinterpret_cast<const uint4*>(series + base);
             u4 = *reinterpret_cast<const uint4*>(values + base);
@@ -464,11 +487,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         }
       }
 #pragma unroll
-      for (int g = 0; g < PH; g += 4) {
-        uint32_t pl[4];
+      for (int g = 0; g < PH; g += GS) {
+        uint32_t pl[GS];
         uint32_t escm = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < GS; ++q) {
           // fast: +0 <= f < V_ESC, one integer compare of the bit pattern (-0, NaN and
           // (-1, 0) take the exact slow path, which also truncates them to 0)
           const float f = fv[g + q];
@@ -478,36 +501,40 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           if (full) bad |= sv[g + q] >= S;
         }
         if (__ballot(escm != 0u)) {
-          // one copy of the full search in the loop's code: slot q picked by selects
+          // one copy of the full search in the loop's code: slot q's sample is re-read
+          // from the batch (an L2 hit; the 4 slots of a group are consecutive samples).
+          // Picking it from the registers by a dynamic q made the compiler keep sv / fv
+          // in scratch: 24 scratch stores per thread per sub-chunk, each behind a wait
+          // for its load, on every sub-chunk (round 5).
 #pragma unroll 1
-          for (int q = 0; q < 4; ++q) {
-            const uint32_t sq = q == 0 ? sv[g] : q == 1 ? sv[g + 1] : q == 2 ? sv[g + 2] : sv[g + 3];
-            const float fq = q == 0 ? fv[g] : q == 1 ? fv[g + 1] : q == 2 ? fv[g + 2] : fv[g + 3];
-            uint32_t r = 0;
-            if ((escm >> q) & 1u) r = payload1_slow(sq, fq, tb, pass == 0 ? sumfix : nullptr);
+          for (int q = 0; q < GS; ++q) {
             if ((escm >> q) & 1u) {
-              pl[0] = q == 0 ? r : pl[0];
-              pl[1] = q == 1 ? r : pl[1];
-              pl[2] = q == 2 ? r : pl[2];
-              pl[3] = q == 3 ? r : pl[3];
+              const uint32_t i = cl + 4u * ((uint32_t)(h * (PH / 4) + (g + q) / 4) * NT + threadIdx.x) + (uint32_t)(q & 3);
+              const uint32_t r = payload1_slow(series[i], values[i], tb, pass == 0 ? sumfix : nullptr);
+#pragma unroll
+              for (int u = 0; u < GS; ++u) pl[u] = q == u ? r : pl[u];
             }
           }
         }
         // (The LUT read and the value-sum atomic are branches around the direct slots:
         // an unconditional, branch-free version -- every slot reading the LUT and adding
         // 0 to a spare sum -- was slower, bin1 3.89 -> 3.96 ms, profiles/r04i_ab.txt.)
-        uint2 dv[4], lv[4];
+        uint2 dv[GS], lv[GS];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
+        for (int q = 0; q < GS; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // the bucket LUT, read by the direct slots only
+        for (int q = 0; q < GS; ++q) {  // the bucket LUT, read by the direct slots only
           lv[q] = make_uint2(0u, 0u);
+#ifdef L5DH_LUTALL
+          lv[q] = lut2[lut2_index(pl[q] & 0x1FFFFFu)];
+#else
           if (__builtin_amdgcn_ubfe(dv[q].x, __builtin_amdgcn_ubfe(sv[g + q], TILE_SHIFT, 5), 1) != 0u)
             lv[q] = lut2[lut2_index(pl[q])];
+#endif
         }
-        uint32_t rc4[4];
+        uint32_t rc4[GS];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < GS; ++q) {
           const uint32_t s = sv[g + q];
           const uint32_t tw = __builtin_amdgcn_ubfe(s, TILE_SHIFT, 5);
           const bool direct = s < S && __builtin_amdgcn_ubfe(dv[q].x, tw, 1) != 0u;
@@ -527,9 +554,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
               atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
           }
         }
-        // slots 4 (kk NT + thread) + q of this group kk, as loaded
-        *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4) * NT + threadIdx.x)) =
-            make_uint4(rc4[0], rc4[1], rc4[2], rc4[3]);
+        // slots 4 (kk NT + thread) + q of the 16-B group kk, as loaded
+#pragma unroll
+        for (int j = 0; j < GS / 4; ++j)
+          *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4 + j) * NT + threadIdx.x)) =
+              make_uint4(rc4[4 * j], rc4[4 * j + 1], rc4[4 * j + 2], rc4[4 * j + 3]);
         asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
       }
     }
