@@ -329,7 +329,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 //
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
-// lut2 [1024] uint2, direct sums [255 x 32].
+// lut2 [1024] uint2, direct sums [255 x 32] + a spare word per lane.
 #ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
 __device__ unsigned long long g_phase1[1024 * 8];
 #define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
@@ -359,7 +359,7 @@ constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 constexpr int NT1 = L5DH_RBIN1_NT;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
-  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
+  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + (DSUM_N + 64) * 4;
 }
 
 template <int NT, int CH>
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
-  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
+  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N + 64] direct series value sums, a spare per lane
   __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
@@ -516,23 +516,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
             }
           }
         }
-        // (The LUT read and the value-sum atomic are branches around the direct slots:
-        // an unconditional, branch-free version -- every slot reading the LUT and adding
-        // 0 to a spare sum -- was slower, bin1 3.89 -> 3.96 ms, profiles/r04i_ab.txt.)
+        // Every slot reads the LUT (its index depends on the payload only), so the dw and
+        // LUT reads go out together; the ranks and the direct value sums are then issued as
+        // one batch of LDS atomics with no control flow between them (a slot with nothing
+        // to add adds 0 to a spare word of its lane), and their results are used after the
+        // last one is issued: two LDS round trips per group.  The branchy form (LUT read
+        // and value sum only on direct slots) had an lgkmcnt(0) wait behind every atomic
+        // (round 5).
         uint2 dv[GS], lv[GS];
 #pragma unroll
         for (int q = 0; q < GS; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
 #pragma unroll
-        for (int q = 0; q < GS; ++q) {  // the bucket LUT, read by the direct slots only
-          lv[q] = make_uint2(0u, 0u);
-#ifdef L5DH_LUTALL
-          lv[q] = lut2[lut2_index(pl[q] & 0x1FFFFFu)];
-#else
-          if (__builtin_amdgcn_ubfe(dv[q].x, __builtin_amdgcn_ubfe(sv[g + q], TILE_SHIFT, 5), 1) != 0u)
-            lv[q] = lut2[lut2_index(pl[q])];
-#endif
-        }
-        uint32_t rc4[GS];
+        for (int q = 0; q < GS; ++q) lv[q] = lut2[lut2_index(pl[q] & 0x1FFFFFu)];
+        uint32_t rc4[GS], wrap = 0;
 #pragma unroll
         for (int q = 0; q < GS; ++q) {
           const uint32_t s = sv[g + q];
@@ -543,16 +539,22 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           uint32_t o;
           const uint32_t bk = lut2_decode(p, lv[q], o);
           const bool esc = p >= V_ESC;
-          const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
-          rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
+          const uint32_t bucket = esc ? p - V_ESC : bk;
+          rc4[q] = direct ? ((s & (TILE - 1)) << 11) | bucket : ((s & (ST_TILES * TILE - 1)) << 21) | p;
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
-          const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
-          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
-          if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
-            const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
-            if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
-              atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
-          }
+          const uint32_t bn = s < S ? (direct ? dbin : s >> ST_SHIFT) : TB;
+          // (hot-bin ranking: the rank is counted by wave ballots below, this add is spare)
+          pk[h * PH + g + q] = atomicAdd(hotrank ? dsum + DSUM_N + lane : cnt + bn, 1u) | (bn << 15);
+          const bool dsum_it = direct && !esc && p != 0u && pass == 0;  // the direct series' value sum
+          const uint32_t dadd = dsum_it ? p : 0u;
+          const uint32_t dold =
+              atomicAdd(dsum + (dsum_it ? di * TILE + (s & (TILE - 1)) : (uint32_t)DSUM_N + (uint32_t)lane), dadd);
+          wrap |= dold + dadd < dold ? 1u << q : 0u;  // this add wrapped the u32 sum
+        }
+        if (__ballot(wrap != 0u)) {  // (rare) 2^32 to the wrapped series' sumfix
+#pragma unroll
+          for (int q = 0; q < GS; ++q)
+            if ((wrap >> q) & 1u) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[sv[g + q]]), 1ull << 32);
         }
         // slots 4 (kk NT + thread) + q of the 16-B group kk, as loaded
 #pragma unroll
@@ -566,6 +568,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t wc0 = 0, wc1 = 0;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
+        pk[k] &= ~0x7FFFu;  // (the main loop's spare add left a rank there)
         const uint32_t b = (pk[k] >> 15) & 1023u;
         const bool m0 = b == hb0, m1 = b == hb1;
         wc0 += (uint32_t)__popcll(__ballot(m0));
@@ -620,10 +623,17 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const uint32_t rin = wave_incl_scan32(tr);
       uint32_t r = rin - tr;
       if (lane == 63) nruns = rin;
+      if (lane == 0) gpre[0] = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         offr[16 * lane + q] = e | (r << 16);
-        if (c[q]) atomicOr(&heads[e >> 5], 1u << (e & 31u));
+        if (c[q]) {
+          atomicOr(&heads[e >> 5], 1u << (e & 31u));
+          // runs before group g (entries [64 g, 64 g + 64)) for the groups whose start this
+          // run covers: e < 64 g <= e + c (the next run starts at e + c)
+          for (uint32_t gg = (e >> 6) + 1u; 64u * gg <= e + c[q] && gg < (uint32_t)(CH / 64); ++gg)
+            gpre[gg] = (uint16_t)(r + 1u);
+        }
         e += c[q];
         r += c[q] ? 1u : 0u;
       }
@@ -639,19 +649,17 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #if L5DH_PF  // (after B2: the run reservations' returns and the scan never wait behind these loads)
     if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
 #endif
+    // the scatter: each batch's offset reads go out together, then its stores (the
+    // compiler cannot move a read of offr above a store to the stage -- one array -- so
+    // a read-store pair per slot waited on every read)
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t bin = (pk[k] >> 15) & 1023u;
-      stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
-    }
-    if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
-      const uint32_t at = threadIdx.x * 64u;
-      uint32_t lb = 0, hb = BIN1_BINS;  // first b with offset(b) >= at
-      while (lb < hb) {
-        const uint32_t m = (lb + hb) >> 1;
-        if ((offr[m] & 0xFFFFu) < at) lb = m + 1; else hb = m;
-      }
-      gpre[threadIdx.x] = (uint16_t)(lb < BIN1_BINS ? offr[lb] >> 16 : nruns);
+    for (int k0 = 0; k0 < PT; k0 += 8) {
+      uint32_t o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = offr[(pk[k0 + j] >> 15) & 1023u];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) stage[(o[j] & 0xFFFFu) + (pk[k0 + j] & 0x7FFFu)] = rec[k0 + j];
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
@@ -671,19 +679,33 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
     for (int j = 0; j < RB; ++j)
       if (threadIdx.x + (uint32_t)j * NT < BIN1_BINS) cnt[threadIdx.x + (uint32_t)j * NT] = 0;
-#pragma unroll 4
-    for (int k = 0; k < PT; ++k) {  // all CH entries, in sorted order (each wave a contiguous PT x 64 range)
-      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
-      const uint32_t g = i >> 6;  // (wave-uniform)
-      const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
-      const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
-      const uint32_t d = rdelta[run];
-      if (d != NODEST) {
-        if (run < nst)
-          rec32[i + d] = stage[i];
-        else
-          rec16[i + d] = (uint16_t)stage[i];
+    // all CH entries, in sorted order (each wave a contiguous PT x 64 range), in batches
+    // whose LDS reads go out together (the heads / gpre words are wave-uniform)
+#pragma unroll 1
+    for (int k0 = 0; k0 < PT; k0 += 8) {
+      uint32_t x[8], run[8], d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
+        const uint32_t g = i >> 6;  // (wave-uniform)
+        const uint2 hw2 = *reinterpret_cast<const uint2*>(heads + 2 * g);
+        const unsigned long long hw = ((unsigned long long)hw2.y << 32) | hw2.x;
+        run[j] = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
+        x[j] = stage[i];
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = rdelta[run[j]];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
+        if (d[j] != NODEST) {
+          if (run[j] < nst)
+            rec32[i + d[j]] = x[j];
+          else
+            rec16[i + d[j]] = (uint16_t)x[j];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // (one batch in registers at a time)
     }
     __syncthreads();  // B4
     PH_MARK(3)
@@ -849,10 +871,12 @@ constexpr int B2_KEYS = 2 * ST_TILES;
 // phases overlap the other's: level 2 -1.4 % on C3, -10 % on C2 against one 1024-thread
 // workgroup with 16 K-record items (profiles/r04p_ab.txt)
 constexpr int B2_NT = 512, B2_PER_CU = 2;
-constexpr size_t rbin2_lds() { return 2048 * 8 + LUT2_N * 8 + 2 * B2_KEYS * 8 + B2_KEYS * 4 + 2 * (size_t)ITEM2 * 4; }
+constexpr size_t rbin2_lds() {
+  return 2048 * 8 + LUT2_N * 8 + 2 * B2_KEYS * 8 + (B2_KEYS + 64) * 4 + 2 * (size_t)ITEM2 * 4;
+}
 
 template <int NT>
-__global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
+__global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, uint32_t F, Tables tb, uint32_t* __restrict__ meta,
                                                  const uint32_t* __restrict__ m_is, const uint32_t* __restrict__ m_bb,
                                                  const uint32_t* __restrict__ m_bt,
                                                  const uint32_t* __restrict__ rec32, uint16_t* __restrict__ rec16,
@@ -865,8 +889,8 @@ __global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F,
   unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem);  // [2048]
   uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                     // [LUT2_N]
   uint2* ocx = lut2 + LUT2_N;                                              // [2][B2_KEYS] {stage offset, run base}
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(ocx + 2 * B2_KEYS);          // [B2_KEYS]
-  uint32_t* stage = cnt + B2_KEYS;                                         // [2][ITEM2] {rec16 | key << 16}, sorted
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(ocx + 2 * B2_KEYS);          // [B2_KEYS + 64]: a spare per lane
+  uint32_t* stage = cnt + B2_KEYS + 64;                                    // [2][ITEM2] {rec16 | key << 16}, sorted
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO2]) == 0u) return;
@@ -960,6 +984,11 @@ __global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F,
       for (int g = 0; g < PG; ++g) {
         r[4 * g] = x[g].x; r[4 * g + 1] = x[g].y; r[4 * g + 2] = x[g].z; r[4 * g + 3] = x[g].w;
       }
+      // The rank and value-sum atomics carry no control flow: an invalid slot (past the
+      // item's end) counts into a spare word of its lane and every slot adds to a sum (0
+      // when it has nothing to add), so the atomics of consecutive slots stay in flight
+      // together.  The branchy form (rank = valid ? atomicAdd : 0, sum under an if) had an
+      // lgkmcnt(0) wait behind every rank atomic (round 5).
       constexpr int H = PT / 2;  // LUT reads batched per half (bounded register pressure)
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
@@ -976,10 +1005,8 @@ __global__ __launch_bounds__(NT, B2_PER_CU) void k_rbin2(uint32_t S, uint32_t F,
         const uint32_t sl = (r[k] >> 21) & 31u, tl = r[k] >> 26;
         const bool valid = 4u * ((uint32_t)(k >> 2) * NT + threadIdx.x) + (uint32_t)(k & 3) < ctot;
         kr[k] = valid ? ((sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16)) : NOKEY;
-        // (branches around the atomics: the branch-free form -- an invalid slot adding 0 to
-        // a count, every slot adding to a sum -- was slower, 0.96 -> 1.03 ms, r04j_ab.txt)
-        rank[k] = valid ? atomicAdd(&cnt[kr[k] >> 16], 1u) : 0u;
-        if (pass == 0 && valid && !esc && p) atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)p);
+        rank[k] = atomicAdd(&cnt[valid ? kr[k] >> 16 : (uint32_t)B2_KEYS + (uint32_t)lane], 1u);
+        atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)((pass == 0 && valid && !esc && p) ? p : 0u));
       }
     }
     __syncthreads();  // B1: counts complete

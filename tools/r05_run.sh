@@ -23,4 +23,8 @@ if [ -n "$BENCH" ]; then
     echo "bench $wl: $(python3 -c "import json; d=json.loads(open('$OUT/bench_$wl.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['path_roofline']['frac'], {k: v['avg_ms'] for k, v in d['kernels'].items()})")"
   done
 fi
+if [ -n "$PMC" ]; then  # HBM traffic per launch of the level-1 / level-2 / accumulate kernels
+  PMC_PASSES="FETCH_SIZE;WRITE_SIZE" PMC_KERNELS="rbin|accum" bash tools/profile_pmc.sh $OUT/pmc --steps 2 --warmup 1 --cpu-sample 0 || exit 1
+  python3 tools/pmc_summary.py $OUT/pmc $OUT/pmc.json '{"workload": "c3", "series": 1000000, "samples": 1000000000}' > $OUT/pmc_summary.txt && grep -E "rbin|accum" $OUT/pmc_summary.txt | cut -c1-220
+fi
 echo done
