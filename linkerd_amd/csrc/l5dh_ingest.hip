@@ -385,7 +385,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
   uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N + 64] direct series value sums, a spare per lane
-  __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
@@ -544,7 +543,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = s < S ? (direct ? dbin : s >> ST_SHIFT) : TB;
           // (hot-bin ranking: the rank is counted by wave ballots below, this add is spare)
-          pk[h * PH + g + q] = atomicAdd(hotrank ? dsum + DSUM_N + lane : cnt + bn, 1u) | (bn << 15);
+          pk[h * PH + g + q] = (atomicAdd(hotrank ? dsum + DSUM_N + lane : cnt + bn, 1u) & 0x7FFFu) | (bn << 15);
           const bool dsum_it = direct && !esc && p != 0u && pass == 0;  // the direct series' value sum
           const uint32_t dadd = dsum_it ? p : 0u;
           const uint32_t dold =
@@ -568,7 +567,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t wc0 = 0, wc1 = 0;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        pk[k] &= ~0x7FFFu;  // (the main loop's spare add left a rank there)
+        pk[k] &= ~0x7FFFu;  // (the main loop's spare add left a value there)
         const uint32_t b = (pk[k] >> 15) & 1023u;
         const bool m0 = b == hb0, m1 = b == hb1;
         wc0 += (uint32_t)__popcll(__ballot(m0));
@@ -622,7 +621,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t e = wave_incl_scan32(tl) - tl;
       const uint32_t rin = wave_incl_scan32(tr);
       uint32_t r = rin - tr;
-      if (lane == 63) nruns = rin;
       if (lane == 0) gpre[0] = 0;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -942,17 +940,25 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
     }
   };
   // write-out of a sorted stage (each wave a contiguous range)
+  // (in batches of 4 entries whose LDS reads go out together: entries past the end are
+  // read too -- stale stage words, their key masked into range -- and not stored)
   auto write_out = [&](int bb, uint32_t total) {
     const uint32_t* st = stage + bb * ITEM2;
     const uint2* oc = ocx + bb * B2_KEYS;
-#pragma unroll 4
-    for (int k = 0; k < PT; ++k) {
-      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
-      if (i < total) {
-        const uint32_t x = st[i];
-        const uint2 o = oc[x >> 16];
-        if (o.y != INVALID) rec16[o.y + (i - o.x)] = (uint16_t)(x & 0xFFFFu);
+#pragma unroll
+    for (int k0 = 0; k0 < PT; k0 += 4) {
+      uint32_t x[4];
+      uint2 o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = st[(uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = oc[(x[j] >> 16) & (B2_KEYS - 1)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
+        if (i < total && o[j].y != INVALID) rec16[o[j].y + (i - o[j].x)] = (uint16_t)(x[j] & 0xFFFFu);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   uint32_t j, a, e;
@@ -1033,9 +1039,18 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
     {
       uint32_t* st = stage + b * ITEM2;
       const uint2* oc = ocx + b * B2_KEYS;
+      // (offset reads of 4 slots together, then their stores: the compiler cannot move a
+      // read of ocx above a store to the stage, so a read-store pair per slot waited on
+      // every read)
 #pragma unroll
-      for (int k = 0; k < PT; ++k)
-        if (kr[k] != NOKEY) st[oc[kr[k] >> 16].x + rank[k]] = kr[k];
+      for (int k0 = 0; k0 < PT; k0 += 4) {
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (kr[k0 + j] != NOKEY) st[o[j] + rank[k0 + j]] = kr[k0 + j];
+      }
     }
     // (E) write-out of the previous item (its stage and run offsets are complete)
     if (item > i0) write_out(b ^ 1, prev_total);

@@ -1118,7 +1118,10 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
                               Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st) {
   if (max_split_items == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, (uint32_t)num_cus())), dim3(WG),
+#ifndef L5DH_SPLIT_WG
+#define L5DH_SPLIT_WG 1024
+#endif
+  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(std::min<uint32_t>(max_split_items, (uint32_t)num_cus()), L5DH_SPLIT_WG)), dim3(WG),
                      ACC_SPLIT_LDS, st, segs, plan, state, tb, out, direct_out, hot_chunk);
   return hipGetLastError();
 }
