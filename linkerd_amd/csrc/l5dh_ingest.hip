@@ -95,20 +95,24 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* lds 
 // Sample: key = series >> 4 = 2 tile + half.  LDS: u16 pairs of keys.
 __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ series, size_t n, uint32_t S, uint32_t K,
                                                   uint32_t* __restrict__ kest) {
-  extern __shared__ uint32_t c[];  // [(K + 1) / 2]
-  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) c[i] = 0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t c[];  // [(K + 1) / 2], padded to 16 B
+  const uint32_t W4 = ((K + 1) / 2 + 3) / 4;  // 16-B groups of counter words
+  for (uint32_t i = threadIdx.x; i < W4; i += 1024) reinterpret_cast<uint4*>(c)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
   const uint64_t per = (m + RS_WG - 1) / RS_WG;
   const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
   // evenly spaced single draws (runs of consecutive ids misjudge a structured stream,
-  // e.g. C2's affine permutation), four per thread with their loads in flight together
+  // e.g. C2's affine permutation), four per thread with their loads in flight together;
+  // draw k reads sample floor(k n / m) in 32.32 fixed point (n / m < 2^12 and k < 2^18:
+  // the product fits 64 bits; a 64-bit division per draw before)
+  const uint64_t step = m == n ? 0ull : (((uint64_t)n << 32) / m);
   for (uint64_t kb = k0; kb < k1; kb += 4 * 1024) {
     uint32_t sv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint64_t k = kb + threadIdx.x + 1024u * u;
-      const uint64_t i = m == n ? k : k * n / m;
+      const uint64_t i = m == n ? k : (k * step) >> 32;
       sv[u] = k < k1 ? series[i < n ? i : 0] : 0xFFFFFFFFu;
     }
 #pragma unroll
@@ -119,10 +123,16 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
       }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) {
-    const uint32_t x = c[i];
-    if (x & 0xFFFFu) atomicAdd(&kest[2 * i], x & 0xFFFFu);
-    if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
+  // the flush, 16 B of counters per thread at a time (one LDS read per 4 words)
+  for (uint32_t i4 = threadIdx.x; i4 < W4; i4 += 1024) {
+    const uint4 x4 = reinterpret_cast<const uint4*>(c)[i4];
+    const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = 4 * i4 + (uint32_t)u, x = xs[u];
+      if ((x & 0xFFFFu) && 2 * i < K) atomicAdd(&kest[2 * i], x & 0xFFFFu);
+      if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
+    }
   }
 }
 
@@ -181,10 +191,19 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   __syncthreads();
   auto tile_est = [&](int k) -> uint32_t { return tel[k * 1024 + j]; };  // sampled ids of tile t0 + k
   uint32_t dbits = 0;
-  for (int k = 0; k < 32; ++k) {
-    const double est = (double)tile_est(k) * s;
-    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
-    if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
+  // (the 32 reads of a batch go out before its histogram atomics: a read below an LDS
+  // atomic is not moved above it, so a read-atomic pair per tile waited on every read)
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 8) {
+    uint32_t ev[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ev[k] = tile_est(k0 + k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double est = (double)ev[k] * s;
+      const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
+      if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
+    }
   }
   __syncthreads();
   if (j == 0) {
@@ -1168,7 +1187,7 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
   const uint32_t K = 2 * a.F;
   switch (stage) {
     case 0:  // sample + level-1 plan
-      hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
+      hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)(((K + 1) / 2 + 3) / 4) * 16, st, a.series, a.n, a.S, K,
                          a.kest);
       hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
                          a.dlim16, a.thr_min, a.dmax, a.pct);
