@@ -314,10 +314,8 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_REDO2] = 0;
     hdr[H_HB0] = (b1 >> 10) ? (uint32_t)(b1 & 1023u) : NOKEY;
     hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
-#ifndef L5DH_HSDIV
-#define L5DH_HSDIV 2
-#endif
-    hdr[H_HS] = all > 0 && (b1 >> 10) * L5DH_HSDIV >= all ? 1u : 0u;
+    // (ballots from >= 1/8 of the batch: bin1 3.55 -> 4.11 ms on C3, round 5)
+    hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
@@ -348,7 +346,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 //
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
-// lut2 [1024] uint2, direct sums [255 x 32] + a spare word per lane.
+// lut2 [1024] uint2, direct sums [255 x 32].
 #ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
 __device__ unsigned long long g_phase1[1024 * 8];
 #define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
@@ -378,7 +376,7 @@ constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 constexpr int NT1 = L5DH_RBIN1_NT;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
-  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + (DSUM_N + 64) * 4;
+  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
 }
 
 template <int NT, int CH>
@@ -389,10 +387,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
                                                   uint32_t* __restrict__ err, int vec, int pass) {
   constexpr int PT = CH / NT;  // slots per thread, loaded and ranked in halves
   constexpr int PH = PT / 2;
-#ifndef L5DH_GS
-#define L5DH_GS 4
-#endif
-  constexpr int GS = L5DH_GS;  // slots whose LDS lookups and atomics are issued together
+  constexpr int GS = 4;  // slots per group (a group's LDS lookups go out together)
   static_assert(PH % 4 == 0 && PH % GS == 0 && GS % 4 == 0 && CH <= 32768, "halves of whole 16-B groups; 15-bit ranks");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   uint32_t* stage = smem;                                        // [CH] records, sorted by bin
@@ -403,7 +398,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
-  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N + 64] direct series value sums, a spare per lane
+  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
+  __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
@@ -452,17 +448,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
     const uint32_t cl = c0;
-#ifdef L5DH_H1EARLY  // the second half's loads issued before the first half is ranked
-    uint4 h1s[PH / 4], h1v[PH / 4];
-    if (full) {
-#pragma unroll
-      for (int k = 0; k < PH / 4; ++k) {
-        const uint32_t base = cl + 4u * ((uint32_t)(PH / 4 + k) * NT + threadIdx.x);
-        h1s[k] = *reinterpret_cast<const uint4*>(series + base);
-        h1v[k] = *reinterpret_cast<const uint4*>(values + base);
-      }
-    }
-#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       uint32_t sv[PH];
@@ -476,11 +461,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           if (h < L5DH_PF) {
             s4 = pfs[h * (PH / 4) + k];
             u4 = pfv[h * (PH / 4) + k];
-#ifdef L5DH_H1EARLY
-          } else if (h == 1) {
-            s4 = h1s[k];
-            u4 = h1v[k];
-#endif
           } else {
             s4 = *reinterpret_cast<const uint4*>(series + base);
             u4 = *reinterpret_cast<const uint4*>(values + base);
@@ -534,19 +514,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
             }
           }
         }
-        // Every slot reads the LUT (its index depends on the payload only), so the dw and
-        // LUT reads go out together; the ranks and the direct value sums are then issued as
-        // one batch of LDS atomics with no control flow between them (a slot with nothing
-        // to add adds 0 to a spare word of its lane), and their results are used after the
-        // last one is issued: two LDS round trips per group.  The branchy form (LUT read
-        // and value sum only on direct slots) had an lgkmcnt(0) wait behind every atomic
-        // (round 5).
+        // (The LUT read and the value-sum atomic are branches around the direct slots:
+        // an unconditional, branch-free version -- every slot reading the LUT and adding
+        // 0 to a spare sum -- was slower, bin1 3.89 -> 3.96 ms, profiles/r04i_ab.txt.)
         uint2 dv[GS], lv[GS];
 #pragma unroll
         for (int q = 0; q < GS; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
 #pragma unroll
-        for (int q = 0; q < GS; ++q) lv[q] = lut2[lut2_index(pl[q] & 0x1FFFFFu)];
-        uint32_t rc4[GS], wrap = 0;
+        for (int q = 0; q < GS; ++q) {  // the bucket LUT, read by the direct slots only
+          lv[q] = make_uint2(0u, 0u);
+          if (__builtin_amdgcn_ubfe(dv[q].x, __builtin_amdgcn_ubfe(sv[g + q], TILE_SHIFT, 5), 1) != 0u)
+            lv[q] = lut2[lut2_index(pl[q])];
+        }
+        uint32_t rc4[GS];
 #pragma unroll
         for (int q = 0; q < GS; ++q) {
           const uint32_t s = sv[g + q];
@@ -557,22 +537,16 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           uint32_t o;
           const uint32_t bk = lut2_decode(p, lv[q], o);
           const bool esc = p >= V_ESC;
-          const uint32_t bucket = esc ? p - V_ESC : bk;
-          rc4[q] = direct ? ((s & (TILE - 1)) << 11) | bucket : ((s & (ST_TILES * TILE - 1)) << 21) | p;
+          const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
+          rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
-          const uint32_t bn = s < S ? (direct ? dbin : s >> ST_SHIFT) : TB;
-          // (hot-bin ranking: the rank is counted by wave ballots below, this add is spare)
-          pk[h * PH + g + q] = (atomicAdd(hotrank ? dsum + DSUM_N + lane : cnt + bn, 1u) & 0x7FFFu) | (bn << 15);
-          const bool dsum_it = direct && !esc && p != 0u && pass == 0;  // the direct series' value sum
-          const uint32_t dadd = dsum_it ? p : 0u;
-          const uint32_t dold =
-              atomicAdd(dsum + (dsum_it ? di * TILE + (s & (TILE - 1)) : (uint32_t)DSUM_N + (uint32_t)lane), dadd);
-          wrap |= dold + dadd < dold ? 1u << q : 0u;  // this add wrapped the u32 sum
-        }
-        if (__ballot(wrap != 0u)) {  // (rare) 2^32 to the wrapped series' sumfix
-#pragma unroll
-          for (int q = 0; q < GS; ++q)
-            if ((wrap >> q) & 1u) atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[sv[g + q]]), 1ull << 32);
+          const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
+          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
+          if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
+            const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
+            if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
+              atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
+          }
         }
         // slots 4 (kk NT + thread) + q of the 16-B group kk, as loaded
 #pragma unroll
@@ -586,7 +560,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t wc0 = 0, wc1 = 0;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
-        pk[k] &= ~0x7FFFu;  // (the main loop's spare add left a value there)
         const uint32_t b = (pk[k] >> 15) & 1023u;
         const bool m0 = b == hb0, m1 = b == hb1;
         wc0 += (uint32_t)__popcll(__ballot(m0));
@@ -640,17 +613,11 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t e = wave_incl_scan32(tl) - tl;
       const uint32_t rin = wave_incl_scan32(tr);
       uint32_t r = rin - tr;
-      if (lane == 0) gpre[0] = 0;
+      if (lane == 63) nruns = rin;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         offr[16 * lane + q] = e | (r << 16);
-        if (c[q]) {
-          atomicOr(&heads[e >> 5], 1u << (e & 31u));
-          // runs before group g (entries [64 g, 64 g + 64)) for the groups whose start this
-          // run covers: e < 64 g <= e + c (the next run starts at e + c)
-          for (uint32_t gg = (e >> 6) + 1u; 64u * gg <= e + c[q] && gg < (uint32_t)(CH / 64); ++gg)
-            gpre[gg] = (uint16_t)(r + 1u);
-        }
+        if (c[q]) atomicOr(&heads[e >> 5], 1u << (e & 31u));
         e += c[q];
         r += c[q] ? 1u : 0u;
       }
@@ -666,17 +633,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #if L5DH_PF  // (after B2: the run reservations' returns and the scan never wait behind these loads)
     if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
 #endif
-    // the scatter: each batch's offset reads go out together, then its stores (the
-    // compiler cannot move a read of offr above a store to the stage -- one array -- so
-    // a read-store pair per slot waited on every read)
 #pragma unroll
-    for (int k0 = 0; k0 < PT; k0 += 8) {
-      uint32_t o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = offr[(pk[k0 + j] >> 15) & 1023u];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) stage[(o[j] & 0xFFFFu) + (pk[k0 + j] & 0x7FFFu)] = rec[k0 + j];
-      __builtin_amdgcn_sched_barrier(0);
+    for (int k = 0; k < PT; ++k) {
+      const uint32_t bin = (pk[k] >> 15) & 1023u;
+      stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
+    }
+    if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
+      const uint32_t at = threadIdx.x * 64u;
+      uint32_t lb = 0, hb = BIN1_BINS;  // first b with offset(b) >= at
+      while (lb < hb) {
+        const uint32_t m = (lb + hb) >> 1;
+        if ((offr[m] & 0xFFFFu) < at) lb = m + 1; else hb = m;
+      }
+      gpre[threadIdx.x] = (uint16_t)(lb < BIN1_BINS ? offr[lb] >> 16 : nruns);
     }
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
@@ -696,33 +665,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
     for (int j = 0; j < RB; ++j)
       if (threadIdx.x + (uint32_t)j * NT < BIN1_BINS) cnt[threadIdx.x + (uint32_t)j * NT] = 0;
-    // all CH entries, in sorted order (each wave a contiguous PT x 64 range), in batches
-    // whose LDS reads go out together (the heads / gpre words are wave-uniform)
-#pragma unroll 1
-    for (int k0 = 0; k0 < PT; k0 += 8) {
-      uint32_t x[8], run[8], d[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
-        const uint32_t g = i >> 6;  // (wave-uniform)
-        const uint2 hw2 = *reinterpret_cast<const uint2*>(heads + 2 * g);
-        const unsigned long long hw = ((unsigned long long)hw2.y << 32) | hw2.x;
-        run[j] = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
-        x[j] = stage[i];
+#pragma unroll 4
+    for (int k = 0; k < PT; ++k) {  // all CH entries, in sorted order (each wave a contiguous PT x 64 range)
+      const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
+      const uint32_t g = i >> 6;  // (wave-uniform)
+      const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
+      const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
+      const uint32_t d = rdelta[run];
+      if (d != NODEST) {
+        if (run < nst)
+          rec32[i + d] = stage[i];
+        else
+          rec16[i + d] = (uint16_t)stage[i];
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = rdelta[run[j]];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
-        if (d[j] != NODEST) {
-          if (run[j] < nst)
-            rec32[i + d[j]] = x[j];
-          else
-            rec16[i + d[j]] = (uint16_t)x[j];
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // (one batch in registers at a time)
     }
     __syncthreads();  // B4
     PH_MARK(3)
