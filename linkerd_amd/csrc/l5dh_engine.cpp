@@ -425,21 +425,16 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode =
     HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, c->stream));
   }
   {
-    // cold tiles on the side stream, concurrently with the big tiles (disjoint
-    // tiles and series; the side stream joins back before anything reads them)
+    // the big tiles first (on at most half the CUs), the cold tiles on the side stream
+    // concurrently (disjoint tiles and series; the side stream joins back before anything
+    // reads them)
     KTimer kt(c, L5DH_K_ACCUM);
     if (split_items) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-#ifdef L5DH_SPLIT_FIRST
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-#else
-      HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
-      HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
-#endif
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     } else {
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));

@@ -95,24 +95,20 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* lds 
 // Sample: key = series >> 4 = 2 tile + half.  LDS: u16 pairs of keys.
 __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ series, size_t n, uint32_t S, uint32_t K,
                                                   uint32_t* __restrict__ kest) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t c[];  // [(K + 1) / 2], padded to 16 B
-  const uint32_t W4 = ((K + 1) / 2 + 3) / 4;  // 16-B groups of counter words
-  for (uint32_t i = threadIdx.x; i < W4; i += 1024) reinterpret_cast<uint4*>(c)[i] = make_uint4(0u, 0u, 0u, 0u);
+  extern __shared__ uint32_t c[];  // [(K + 1) / 2]
+  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) c[i] = 0;
   __syncthreads();
   const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
   const uint64_t per = (m + RS_WG - 1) / RS_WG;
   const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
   // evenly spaced single draws (runs of consecutive ids misjudge a structured stream,
-  // e.g. C2's affine permutation), four per thread with their loads in flight together;
-  // draw k reads sample floor(k n / m) in 32.32 fixed point (n / m < 2^12 and k < 2^18:
-  // the product fits 64 bits; a 64-bit division per draw before)
-  const uint64_t step = m == n ? 0ull : (((uint64_t)n << 32) / m);
+  // e.g. C2's affine permutation), four per thread with their loads in flight together
   for (uint64_t kb = k0; kb < k1; kb += 4 * 1024) {
     uint32_t sv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint64_t k = kb + threadIdx.x + 1024u * u;
-      const uint64_t i = m == n ? k : (k * step) >> 32;
+      const uint64_t i = m == n ? k : k * n / m;
       sv[u] = k < k1 ? series[i < n ? i : 0] : 0xFFFFFFFFu;
     }
 #pragma unroll
@@ -123,16 +119,10 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
       }
   }
   __syncthreads();
-  // the flush, 16 B of counters per thread at a time (one LDS read per 4 words)
-  for (uint32_t i4 = threadIdx.x; i4 < W4; i4 += 1024) {
-    const uint4 x4 = reinterpret_cast<const uint4*>(c)[i4];
-    const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t i = 4 * i4 + (uint32_t)u, x = xs[u];
-      if ((x & 0xFFFFu) && 2 * i < K) atomicAdd(&kest[2 * i], x & 0xFFFFu);
-      if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
-    }
+  for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) {
+    const uint32_t x = c[i];
+    if (x & 0xFFFFu) atomicAdd(&kest[2 * i], x & 0xFFFFu);
+    if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
   }
 }
 
@@ -191,19 +181,10 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   __syncthreads();
   auto tile_est = [&](int k) -> uint32_t { return tel[k * 1024 + j]; };  // sampled ids of tile t0 + k
   uint32_t dbits = 0;
-  // (the 32 reads of a batch go out before its histogram atomics: a read below an LDS
-  // atomic is not moved above it, so a read-atomic pair per tile waited on every read)
-#pragma unroll
-  for (int k0 = 0; k0 < 32; k0 += 8) {
-    uint32_t ev[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ev[k] = tile_est(k0 + k);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const double est = (double)ev[k] * s;
-      const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
-      if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
-    }
+  for (int k = 0; k < 32; ++k) {
+    const double est = (double)tile_est(k) * s;
+    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
+    if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
   }
   __syncthreads();
   if (j == 0) {
@@ -366,7 +347,13 @@ __device__ unsigned long long g_phase1[1024 * 8];
 #define PH_MARK(k)
 #define PH_FLUSH
 #endif
+#ifdef L5DH_DSUM64
+constexpr int CHW = 16384;  // (u64 direct sums: 16 slots per thread)
+using dsum_t = unsigned long long;
+#else
 constexpr int CHW = 24576;
+using dsum_t = uint32_t;
+#endif
 // rdelta of a dropped run: a valid delta (run base - stage offset) lies in (-CHW, cap16),
 // cap16 < 2^32 - CHW - 1, so -(CHW + 1) never is one (0xFFFFFFFF is: base 0 at offset 1)
 constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
@@ -376,7 +363,7 @@ constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
 constexpr int NT1 = L5DH_RBIN1_NT;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
-  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * 4;
+  return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * sizeof(dsum_t);
 }
 
 template <int NT, int CH>
@@ -398,7 +385,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
-  uint32_t* dsum = reinterpret_cast<uint32_t*>(lut2 + LUT2_N);   // [DSUM_N] direct series value sums
+  dsum_t* dsum = reinterpret_cast<dsum_t*>(lut2 + LUT2_N);       // [DSUM_N] direct series value sums
   __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
@@ -542,11 +529,15 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
           pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
+#ifdef L5DH_DSUM64
+          if (direct && !esc && p != 0u && pass == 0) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], (dsum_t)p);
+#else
           if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
             const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
             if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
               atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
           }
+#endif
         }
         // slots 4 (kk NT + thread) + q of the 16-B group kk, as loaded
 #pragma unroll
@@ -1142,7 +1133,7 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
   const uint32_t K = 2 * a.F;
   switch (stage) {
     case 0:  // sample + level-1 plan
-      hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)(((K + 1) / 2 + 3) / 4) * 16, st, a.series, a.n, a.S, K,
+      hipLaunchKernelGGL(k_rsample, dim3(RS_WG), dim3(1024), (size_t)((K + 1) / 2) * 4, st, a.series, a.n, a.S, K,
                          a.kest);
       hipLaunchKernelGGL(k_rplan1, dim3(1), dim3(1024), RPLAN1_LDS, st, a.n, a.F, a.kest, a.kprev, a.meta, a.cap32,
                          a.dlim16, a.thr_min, a.dmax, a.pct);

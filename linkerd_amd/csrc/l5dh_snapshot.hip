@@ -646,33 +646,15 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
       PH_MARK(1)
       uint4* o = reinterpret_cast<uint4*>(out.counts + (size_t)oi0 * NB);
       constexpr int NCH = HSER * NB / 4;
-      // 4 chunks per thread at a time: their LDS reads go out together, then the stores
-      // and the clears (a clear is a store to the words just read, so the compiler could
-      // not move the next chunk's reads above it: one LDS round trip per chunk)
-      constexpr int CB = 4;
-      for (int c0 = threadIdx.x; c0 < NCH; c0 += CB * NT) {
-        uint32_t* p0[CB];
-        uint32_t* p1[CB];
-        uint32_t x[CB], y[CB];
-#pragma unroll
-        for (int j = 0; j < CB; ++j) {
-          const int c = min(c0 + j * NT, NCH - 1);  // (a chunk past the end re-reads the last one)
-          const int e0 = 4 * c;
-          const int r0 = e0 / NB, b0 = e0 - r0 * NB;
-          p0[j] = hist + r0 * CROW + (b0 >> 1);
-          p1[j] = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0[j] + 1;
-          x[j] = *p0[j];
-          y[j] = *p1[j];
-        }
-#pragma unroll
-        for (int j = 0; j < CB; ++j) {
-          const int c = c0 + j * NT;
-          if (c < NCH) {  // (a re-read chunk is neither stored nor cleared: its own thread does both)
-            o[c] = make_uint4(x[j] & 0xFFFFu, x[j] >> 16, y[j] & 0xFFFFu, y[j] >> 16);
-            *p0[j] = 0u;
-            *p1[j] = 0u;
-          }
-        }
+      for (int c = threadIdx.x; c < NCH; c += NT) {
+        const int e0 = 4 * c;
+        const int r0 = e0 / NB, b0 = e0 - r0 * NB;
+        uint32_t* p0 = hist + r0 * CROW + (b0 >> 1);
+        uint32_t* p1 = b0 == NB - 2 ? hist + (r0 + 1) * CROW : p0 + 1;
+        const uint32_t x = *p0, y = *p1;
+        *p0 = 0u;
+        *p1 = 0u;
+        o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
       }
     }
     if (threadIdx.x == 0) {
@@ -899,20 +881,12 @@ __global__ __launch_bounds__(WG) void k_accum_split(Segs segs, Plan plan, State 
       const BigRows br = big_rows(st, out, plan, t, direct_out);
       uint32_t* grow = br.base + (size_t)(16 * half + w) * br.stride;
       const uint32_t* hrow = hist + w * HROW;
-      // 64 consecutive bins per wave atomic; the LDS reads of 8 such stretches go out
-      // together (a read, a wait and the ballot's branch per stretch before)
-      for (int b00 = 0; b00 < NB; b00 += 8 * 64) {
-        uint32_t v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int b = b00 + 64 * j + lane;
-          v[j] = b < NB ? hrow[b] : 0u;
+      for (int b0 = 0; b0 < NB; b0 += 64) {  // 64 consecutive bins per wave atomic
+        const int b = b0 + lane;
+        const uint32_t v = b < NB ? hrow[b] : 0u;
+        if (__ballot(v != 0u)) {
+          if (v) atomicAdd(&grow[b], v);
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (__ballot(v[j] != 0u)) {
-            if (v[j]) atomicAdd(&grow[b00 + 64 * j + lane], v[j]);
-          }
       }
     }
     if (threadIdx.x == 0) s_item = gridDim.x + atomicAdd(ctr, 1u);
@@ -1144,10 +1118,11 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
                               Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st) {
   if (max_split_items == 0) return hipSuccess;
-#ifndef L5DH_SPLIT_WG
-#define L5DH_SPLIT_WG 1024
-#endif
-  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(std::min<uint32_t>(max_split_items, (uint32_t)num_cus()), L5DH_SPLIT_WG)), dim3(WG),
+  // at most half the CUs: launched before the cold tiles' kernel, it leaves the other
+  // half to it (k_accum_split takes 115 KB of LDS: the two cannot share a CU), and its
+  // workgroups and the cold ones take items until both queues are empty (accumulate
+  // phase 1.67 -> 1.63 ms on C3 against every CU first, round 5)
+  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, (uint32_t)num_cus() / 2)), dim3(WG),
                      ACC_SPLIT_LDS, st, segs, plan, state, tb, out, direct_out, hot_chunk);
   return hipGetLastError();
 }
