@@ -140,8 +140,6 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   __shared__ uint64_t l64[17];
   __shared__ uint32_t dl[DIRECT_MAX + 1];
   __shared__ uint32_t capl[BIN1_BINS];
-  __shared__ double predl[BIN1_BINS];
-  __shared__ unsigned long long best[16];
   extern __shared__ uint32_t tel[];  // [32][1024]: sampled ids of tile t0 + k at tel[k * 1024 + j]
   const MetaLayout L = meta_layout(F);
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
@@ -152,7 +150,6 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   const uint32_t j = threadIdx.x, t0 = j * 32;
   if (j < 33) lh[j] = 0;
   capl[j] = 0;
-  predl[j] = 0.0;
   // this thread's 32 tiles (64 consecutive key words) read once, all 16-B loads in
   // flight together (a ragged end word by word), kept in LDS for the passes below
   auto tile_pairs = [&](const uint32_t* __restrict__ kw, auto&& put) {
@@ -237,7 +234,6 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   if ((j & 1u) == 0 && (j >> 1) < FS) {
     const uint32_t b = j >> 1;
     capl[b] = rcap(P, E, s, exact, 256.0, 4, pct);
-    predl[b] = fmax(P, E * s);
   }
   __syncthreads();  // dl complete
   const uint32_t TB = FS + 2 * ND;
@@ -245,7 +241,6 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     const uint32_t t = dl[(j - FS) >> 1], h = (j - FS) & 1u;
     const double p = (double)kprev[2 * t + h], e = (double)kest[2 * t + h];
     capl[j] = rcap(p, e, s, exact, 256.0, 8, pct);  // (u16 records: 16-B aligned regions)
-    predl[j] = fmax(p, e * s);
   }
   __syncthreads();
   // two address spaces: super-tile bins in rec32, the direct half-bins in rec16 below
@@ -261,55 +256,25 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   meta[L.bbase() + j] = (uint32_t)base;
   meta[L.bcap() + j] = j < TB ? capl[j] : 0u;
   meta[L.bcnt() + j] = 0u;
-  // the two biggest bins by prediction, for the ballot ranking of k_rbin1w
-  const int lane = j & 63, w = j >> 6;
-  auto block_max = [&](unsigned long long v) -> unsigned long long {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      const unsigned long long o = __shfl_xor(v, d, 64);
-      v = o > v ? o : v;
-    }
-    __syncthreads();
-    if (lane == 0) best[w] = v;
-    __syncthreads();
-    unsigned long long r = 0;
-    for (int q = 0; q < 16; ++q) r = best[q] > r ? best[q] : r;
-    return r;
-  };
-  const unsigned long long mine = j < TB ? (((unsigned long long)fmin(predl[j], 4.0e12) << 10) | j) : 0ull;
-  const unsigned long long b1 = block_max(mine);
-  const unsigned long long b2 = block_max(mine == b1 ? 0ull : mine);
-  double psum = j < TB ? predl[j] : 0.0;
-  psum = (double)wave_sum((uint64_t)psum);
-  __syncthreads();
-  if (lane == 0) best[w] = (unsigned long long)psum;
-  __syncthreads();
   if (j == 0) {
-    unsigned long long all = 0;
-    for (int q = 0; q < 16; ++q) all += best[q];
     uint32_t* hdr = meta + L.hdr();
     hdr[H_ND] = ND;
     hdr[H_OV1] = 0;
     hdr[H_REDO1] = 0;
     hdr[H_OV2] = 0;
     hdr[H_REDO2] = 0;
-    hdr[H_HB0] = (b1 >> 10) ? (uint32_t)(b1 & 1023u) : NOKEY;
-    hdr[H_HB1] = (b2 >> 10) ? (uint32_t)(b2 & 1023u) : NOKEY;
-    // (ballots from >= 1/8 of the batch: bin1 3.55 -> 4.11 ms on C3, round 5)
-    hdr[H_HS] = all > 0 && (b1 >> 10) * 2 >= all ? 1u : 0u;
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
 }
 
 // ------------------------------------------------------------------------
-// Level 1, one 1024-thread workgroup per CU walking its slab in 24K-slot sub-chunks.
+// Level 1, one 1024-thread workgroup per CU walking its slab in 16K-slot sub-chunks.
 // Bins: the FS super-tiles (u32 records with the value, for level 2), two half-bins
 // per direct tile (final u16 records: the sample is bucketized here, and its value
 // added to an LDS sum of its series), and a trash bin (slots with no valid sample:
 // the batch's ragged end, ids >= S) that is never written.  Per sub-chunk: one LDS
-// atomic ranks each slot in its bin (or a wave ballot, for the two hottest bins when
-// one holds >= half the batch), one returning global atomic per non-empty bin
+// atomic ranks each slot in its bin, one returning global atomic per non-empty bin
 // reserves the sub-chunk's run in the bin's region, a one-wave scan gives stage
 // offsets and run ranks, the records are staged sorted (4 B each), and the stage is
 // written out in order: each entry's run is the number of run heads at or before
@@ -321,13 +286,19 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // profiles/r04r_ab.txt, r04s_ab.txt).  A run that does not fit is dropped and flagged; pass 1 (the redo) exits unless k_rfix1 asked for it and adds nothing to
 // sumfix or the error counter.
 //
-// Direct value sums: u32 per direct series in LDS; an add that wraps past 2^32 adds
-// 2^32 to sumfix[series] (the wrapping lane is told by the atomic's return value),
-// and each workgroup adds its remainders to sumfix at the end of its slab.
+// Direct value sums: u64 per direct series in LDS, added to sumfix by each workgroup at
+// the end of its slab.
+//
+// No LDS atomic of the ranking loop is under a branch that its return value or a
+// uniform flag decides: the compiler then waits for each return before the next slot
+// (s_waitcnt lgkmcnt(0) after every atomic).  Unconditional rank atomics and return-less
+// u64 value sums keep a group's 8 atomics in flight together: bin1 3.56 -> 3.36 ms on C3
+// (profiles/r05k_level1_atomics_ab.txt).  16 K-slot sub-chunks (16 slots per thread)
+// leave the VGPRs for that (24 K spills the prefetch: 3.94 ms) and the LDS for the u64 sums.
 //
 // LDS (u32 words): stage[CH], cnt[1024], offr[1024] {offset | run rank << 16},
 // rdelta[1024], heads[CH / 32], gpre[CH / 64] (u16), direct words [1024] uint2,
-// lut2 [1024] uint2, direct sums [255 x 32].
+// lut2 [1024] uint2, direct sums [255 x 32] u64.
 #ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
 __device__ unsigned long long g_phase1[1024 * 8];
 #define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
@@ -347,14 +318,12 @@ __device__ unsigned long long g_phase1[1024 * 8];
 #define PH_MARK(k)
 #define PH_FLUSH
 #endif
-constexpr int CHW = 24576;
-// (u64 LDS sums with 16 K-sample sub-chunks -- no wrap check, no returning atomic -- measured
-// level 1 3.55 vs 3.55 ms on C3, round 5: the u32 sums stay, with 50 % longer runs per bin)
-using dsum_t = uint32_t;
+constexpr int CHW = 16384;
+using dsum_t = unsigned long long;
 // rdelta of a dropped run: a valid delta (run base - stage offset) lies in (-CHW, cap16),
 // cap16 < 2^32 - CHW - 1, so -(CHW + 1) never is one (0xFFFFFFFF is: base 0 at offset 1)
 constexpr uint32_t NODEST = 0xFFFFFFFFu - (uint32_t)CHW;
-constexpr int NT1 = 1024;  // 24 slots per thread (1024 threads: -0.6 ms on C3 against 768 x 32, r04d)
+constexpr int NT1 = 1024;  // 16 slots per thread
 constexpr int DSUM_N = DIRECT_MAX * TILE;
 constexpr size_t rbin1w_lds() {
   return (size_t)CHW * 4 + BIN1_BINS * 12 + CHW / 8 + CHW / 32 + 1024 * 8 + LUT2_N * 8 + DSUM_N * sizeof(dsum_t);
@@ -391,8 +360,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t NW = (F + 31) / 32;
   const uint32_t ND = hdr[H_ND];
   const uint32_t TB = FS + 2 * ND;
-  const bool hotrank = hdr[H_HS] != 0u;
-  const uint32_t hb0 = hdr[H_HB0], hb1 = hdr[H_HB1];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const unsigned long long mle = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
@@ -513,12 +480,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           rc4[q] = sel_u32(direct, ((s & (TILE - 1)) << 11) | bucket, ((s & (ST_TILES * TILE - 1)) << 21) | p);
           const uint32_t dbin = FS + 2u * di + ((s >> 4) & 1u);
           const uint32_t bn = sel_u32(s < S, sel_u32(direct, dbin, s >> ST_SHIFT), TB);
-          pk[h * PH + g + q] = hotrank ? bn << 15 : atomicAdd(cnt + bn, 1u) | (bn << 15);
-          if (direct && !esc && p != 0u && pass == 0) {  // the direct series' value sum
-            const uint32_t old = atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], p);
-            if (old + p < old)  // this add wrapped the u32 sum: 2^32 to the series' sumfix
-              atomicAdd(reinterpret_cast<unsigned long long*>(&sumfix[s]), 1ull << 32);
-          }
+          pk[h * PH + g + q] = atomicAdd(cnt + bn, 1u) | (bn << 15);
+          // the direct series' value sum (u64: no wrap to check, so nothing reads the return)
+          if (direct && !esc && pass == 0 && p) atomicAdd(&dsum[di * TILE + (s & (TILE - 1))], (dsum_t)p);
         }
         // slots 4 (kk NT + thread) + q of the 16-B group kk, as loaded
 #pragma unroll
@@ -526,31 +490,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           *reinterpret_cast<uint4*>(stage + 4u * ((uint32_t)(h * (PH / 4) + g / 4 + j) * NT + threadIdx.x)) =
               make_uint4(rc4[4 * j], rc4[4 * j + 1], rc4[4 * j + 2], rc4[4 * j + 3]);
         asm volatile("" ::: "memory");  // keep the groups apart (bounded register pressure)
-      }
-    }
-    if (hotrank) {
-      uint32_t wc0 = 0, wc1 = 0;
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const uint32_t b = (pk[k] >> 15) & 1023u;
-        const bool m0 = b == hb0, m1 = b == hb1;
-        wc0 += (uint32_t)__popcll(__ballot(m0));
-        wc1 += (uint32_t)__popcll(__ballot(m1));
-        if (!m0 && !m1) pk[k] |= atomicAdd(cnt + b, 1u);
-      }
-      uint32_t base = 0;
-      if (lane == 0 && wc0) base = atomicAdd(cnt + hb0, wc0);
-      if (lane == 1 && wc1) base = atomicAdd(cnt + hb1, wc1);
-      uint32_t r0 = __builtin_amdgcn_readlane(base, 0), r1 = __builtin_amdgcn_readlane(base, 1);
-#pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        const uint32_t b = (pk[k] >> 15) & 1023u;
-        const bool m0 = b == hb0, m1 = b == hb1;
-        const unsigned long long x0 = __ballot(m0), x1 = __ballot(m1);
-        if (m0) pk[k] |= r0 + mask_below(x0);
-        if (m1) pk[k] |= r1 + mask_below(x1);
-        r0 += (uint32_t)__popcll(x0);
-        r1 += (uint32_t)__popcll(x1);
       }
     }
     __syncthreads();  // B1: counts complete

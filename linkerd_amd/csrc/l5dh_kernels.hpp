@@ -88,9 +88,7 @@ enum : uint32_t {
   H_OV2 = 3,      // a level-2 run did not fit its region
   H_REDO2 = 4,    // level 2 runs again with exact regions
   H_ITEMS = 5,    // level-2 items
-  H_HB0 = 6,      // the two hottest level-1 bins (ballot ranking; ~0u: none)
-  H_HB1 = 7,
-  H_HS = 8,       // 1: one bin holds >= half the batch
+  // (6-8: unused)
   H_EXACT = 9,    // 1: every sample of the batch was counted by k_rsample
   H_NOVR1 = 10,   // level-1 redos (diagnostics, monotonic per segment slot)
   H_NOVR2 = 11,
