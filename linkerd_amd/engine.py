@@ -104,8 +104,11 @@ class HistogramEngine:
         """Order the context's next work after everything queued on torch's current
         stream (an event handoff: no host synchronization)."""
         import torch
+        cur = torch.cuda.current_stream(self.device)
+        if self._stream is not None and int(self._stream) == cur.cuda_stream:
+            return  # the context runs on that stream: already in order (a wait would only idle the GPU)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        ev.record(cur)
         self._check(self._lib.l5dh_wait_event(self._ctx, ev.cuda_event), "l5dh_wait_event")
         self._events.append(ev)  # the handle must outlive the enqueued wait
         del self._events[:-4]
