@@ -349,7 +349,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
   dsum_t* dsum = reinterpret_cast<dsum_t*>(lut2 + LUT2_N);       // [DSUM_N] direct series value sums
-  __shared__ uint32_t nruns;
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
   if (pass == 1 && __builtin_amdgcn_readfirstlane(hdr[H_REDO1]) == 0u) return;
@@ -404,7 +403,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           if (h == 0) {
             s4 = pfs[h * (PH / 4) + k];
             u4 = pfv[h * (PH / 4) + k];
-          } else {
+          } else {  // (issued here: in flight during the first half's ranking, they spill registers;
+                    // a timing-only build that skips them saved 0.1 ms of bin1, round 5)
             s4 = *reinterpret_cast<const uint4*>(series + base);
             u4 = *reinterpret_cast<const uint4*>(values + base);
           }
@@ -524,7 +524,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       uint32_t e = wave_incl_scan32(tl) - tl;
       const uint32_t rin = wave_incl_scan32(tr);
       uint32_t r = rin - tr;
-      if (lane == 63) nruns = rin;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         offr[16 * lane + q] = e | (r << 16);
@@ -548,14 +547,23 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const uint32_t bin = (pk[k] >> 15) & 1023u;
       stage[(offr[bin] & 0xFFFFu) + (pk[k] & 0x7FFFu)] = rec[k];
     }
-    if (threadIdx.x < CH / 64) {  // runs before group g = the run rank of the first bin at offset >= 64 g
-      const uint32_t at = threadIdx.x * 64u;
-      uint32_t lb = 0, hb = BIN1_BINS;  // first b with offset(b) >= at
-      while (lb < hb) {
-        const uint32_t m = (lb + hb) >> 1;
-        if ((offr[m] & 0xFFFFu) < at) lb = m + 1; else hb = m;
+    if (wv == 0) {  // runs before group g = run heads in the groups before it (one wave: a scan of popcounts)
+      constexpr int GPL = CH / 64 / 64;  // groups per lane
+      static_assert(GPL % 2 == 0, "two groups per 16-B read");
+      uint32_t pc[GPL], t = 0;
+#pragma unroll
+      for (int k = 0; k < GPL; k += 2) {
+        const uint4 w = *reinterpret_cast<const uint4*>(heads + 2u * (GPL * (uint32_t)lane + (uint32_t)k));
+        pc[k] = (uint32_t)(__popc(w.x) + __popc(w.y));
+        pc[k + 1] = (uint32_t)(__popc(w.z) + __popc(w.w));
+        t += pc[k] + pc[k + 1];
       }
-      gpre[threadIdx.x] = (uint16_t)(lb < BIN1_BINS ? offr[lb] >> 16 : nruns);
+      uint32_t ex = wave_incl_scan32(t) - t;
+#pragma unroll
+      for (int k = 0; k < GPL; ++k) {
+        gpre[GPL * (uint32_t)lane + (uint32_t)k] = (uint16_t)ex;
+        ex += pc[k];
+      }
     }
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
