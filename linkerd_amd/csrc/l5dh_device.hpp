@@ -8,6 +8,7 @@
 // and finagle-stats 6.45.0 BucketedHistogram (percentile/min/max/average), as
 // written out in SURVEY.md §8a.
 #pragma once
+#include <type_traits>
 
 #include "l5dh_kernels.hpp"
 
@@ -74,11 +75,21 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t x) {  // every lane gets t
 __device__ __forceinline__ int lane_groups(int lane) { return lane == 63 ? 9 : 7; }
 
 // Count sources: get4(b0) returns bins b0..b0+3 (b0 % 4 == 0); bins >= 1798 read 0.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// x.lo + x.hi + c (one v_dot2_u32_u16)
+__device__ __forceinline__ uint32_t pair_sum(uint32_t x, uint32_t c) {
+  const u16x2 one = {1, 1};
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), one, c, false);
+}
 struct SrcLds16 {  // u16-packed row in LDS (cold tile: counts of the new records)
   const uint32_t* row;
   __device__ __forceinline__ uint4 get4(int b0) const {
     const uint2 w = *reinterpret_cast<const uint2*>(row + (b0 >> 1));  // word 899 is zero padding
     return make_uint4(w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16);
+  }
+  __device__ __forceinline__ uint32_t sum4(int b0) const {  // bins b0..b0+3 summed, packed
+    const uint2 w = *reinterpret_cast<const uint2*>(row + (b0 >> 1));
+    return pair_sum(w.x, pair_sum(w.y, 0u));
   }
 };
 struct SrcLds32 {  // u32 row in LDS, stride ROW, bins 1798/1799 zero
@@ -127,39 +138,52 @@ __device__ __forceinline__ void store4_state(uint32_t* __restrict__ row, int b0,
 // each reported as the bucket midpoint (mid[0] = 0, mid[1797] = Int.MaxValue).
 // The owner lane of each of the 8 targets is found by ballot over the lane
 // prefix; lanes 0..7 then locate the group (shuffles) and the bin (one get4).
-template <class Src>
+// SMALL: the row's count is below 2^32 (a cold half-tile: <= 65535 records), so the lane
+// prefix, the targets and the owner search are 32-bit (one scan, one readlane, one permute).
+template <class Src, bool SMALL = false>
 __device__ __forceinline__ void wave_summary(const uint32_t (&g)[9], const Src& src, int64_t total,
                                              const int32_t* __restrict__ mid, Summary88* __restrict__ out) {
+  using U = typename std::conditional<SMALL, uint32_t, uint64_t>::type;
+  auto rl = [](U x, int k) -> U {  // lane k's value
+    if constexpr (SMALL) {
+      return (U)__builtin_amdgcn_readlane((uint32_t)x, k);
+    } else {
+      return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), k) << 32) |
+             __builtin_amdgcn_readlane((uint32_t)x, k);
+    }
+  };
   const int lane = lane_id();
-  uint64_t ls = 0;
+  U ls = 0;
 #pragma unroll
   for (int q = 0; q < 9; ++q) ls += g[q];
-  const uint64_t incl = wave_incl_scan(ls);
-  const uint64_t excl = incl - ls;
-  const uint64_t num = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(incl >> 32), 63) << 32) |
-                       __builtin_amdgcn_readlane((uint32_t)incl, 63);
+  U incl;
+  if constexpr (SMALL)
+    incl = wave_incl_scan32(ls);
+  else
+    incl = wave_incl_scan(ls);
+  const U excl = incl - ls;
+  const U num = rl(incl, 63);
   const double dn = (double)num;
 
   // lane k < 8 computes target k (min, p50, p90, p95, p99, p999, p9999, max) in
   // parallel; each target's owner lane is then found with one ballot
-  uint64_t my_t;
+  U my_t;
   {
     const double p = lane == 1 ? 0.50 : lane == 2 ? 0.90 : lane == 3 ? 0.95 : lane == 4 ? 0.99
                    : lane == 5 ? 0.999 : 0.9999;
-    my_t = (uint64_t)java_round_nonneg(__dmul_rn(p, dn));
+    my_t = (U)java_round_nonneg(__dmul_rn(p, dn));
     if (lane == 0) my_t = num ? 1 : 0;
     if (lane >= 7) my_t = num;
   }
   int my_owner = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const uint64_t t = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(my_t >> 32), k) << 32) |
-                       __builtin_amdgcn_readlane((uint32_t)my_t, k);
+    const U t = rl(my_t, k);
     const unsigned long long m = __ballot(t != 0 && excl < t && t <= incl);
     const int owner = m ? (__ffsll((long long)m) - 1) : 0;
     if (lane == k) my_owner = owner;
   }
-  uint64_t acc = __shfl(excl, my_owner, 64);
+  U acc = __shfl(excl, my_owner, 64);
   int qsel = 0;
   bool done = false;
 #pragma unroll

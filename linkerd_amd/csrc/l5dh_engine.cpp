@@ -184,7 +184,7 @@ struct l5dh_ctx {
   uint32_t* d_enc_base = nullptr;  // [F] sparse export: each tile's first word of the unpacked encoding
   uint32_t* d_enc_h0 = nullptr;    // [F] sparse export: words reserved for half 0 of a big or dirty tile
   uint32_t* d_enc_dw = nullptr;    // [2F] sparse export: words of each half of a dirty tile's state rows
-  uint32_t* h_header = nullptr;      // pinned: [4] ingest error count (written by k_rfix1)
+  uint32_t* h_header = nullptr;      // pinned: [4] ingest error count (written by k_rfix1), [5] big tiles of the last plan
   uint32_t* h_header_dev = nullptr;  // its device-side address
   uint32_t* d_kest = nullptr;   // [2F] sampled ids per (tile, half) key of the batch being binned
   uint32_t* d_kprev = nullptr;  // [2F] exact records per key of the previous batch (region sizes)
@@ -360,7 +360,8 @@ State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c-
 
 Plan plan(l5dh_ctx* c) {
   return Plan{c->d_tile_tot, c->d_enc_base, c->d_enc_h0, c->d_enc_dw, c->d_cold_item,
-              static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags, c->d_header};
+              static_cast<uint2*>(c->split_item.p), c->d_hot_list, c->d_tile_flags, c->d_header,
+              c->h_header_dev + 5};
 }
 
 Segs segs_view(l5dh_ctx* c) {
@@ -424,25 +425,30 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode =
     KTimer kt(c, L5DH_K_HOT);
     HIPCHK(c, launch_hot_init(pl, hot, st, out, direct_out, c->stream));
   }
+  bool joined = true;
   {
     // the big tiles first (on at most half the CUs), the cold tiles on the side stream
-    // concurrently (disjoint tiles and series; the side stream joins back before anything
-    // reads them)
+    // concurrently (disjoint tiles and series; the side stream joins back after
+    // k_hot_finish, which touches only big tiles: it runs under the cold kernel)
     KTimer kt(c, L5DH_K_ACCUM);
-    if (split_items) {
+    // The two streams cost ~20 us of idle GPU (the fork's and the join's barrier packets);
+    // they pay only when there are big tiles, so the last plan the host has seen picks the
+    // order (a hint: either order is correct; k_plan_b writes it to a mapped host word)
+    const bool big_seen = __atomic_load_n(c->h_header + 5, __ATOMIC_RELAXED) != 0u;
+    if (split_items && big_seen) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
       HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      joined = false;
     } else {
+      if (split_items) HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));
     }
-  }
-  if (hot) {
-    KTimer kt(c, L5DH_K_HOT);
-    HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, direct_out, c->stream));
+    // (timed with the accumulate: with two streams it runs under the cold kernel)
+    if (hot) HIPCHK(c, launch_hot_finish(pl, hot, st, tb, out, final_mode, reset, direct_out, c->stream));
+    if (!joined) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
   c->nseg = 0;
   return 0;

@@ -275,8 +275,8 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // added to an LDS sum of its series), and a trash bin (slots with no valid sample:
 // the batch's ragged end, ids >= S) that is never written.  Per sub-chunk: one LDS
 // atomic ranks each slot in its bin, one returning global atomic per non-empty bin
-// reserves the sub-chunk's run in the bin's region, a one-wave scan gives stage
-// offsets and run ranks, the records are staged sorted (4 B each), and the stage is
+// reserves the sub-chunk's run in the bin's region, a block scan (one bin per thread)
+// gives stage offsets and run ranks, the records are staged sorted (4 B each), and the stage is
 // written out in order: each entry's run is the number of run heads at or before
 // it -- a per-64-entry group prefix (gpre) plus a popcount of the group's bits of
 // the run-head bitmap -- indexing the runs' destination deltas (rdelta[run] = run
@@ -348,6 +348,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   uint16_t* gpre = reinterpret_cast<uint16_t*>(heads + CH / 32);  // [CH / 64] runs before each 64-entry group
   uint2* dw = reinterpret_cast<uint2*>(gpre + CH / 64);          // [1024] {direct bits, direct tiles before}
   uint2* lut2 = dw + 1024;                                       // [LUT2_N]
+  __shared__ uint32_t wsum[NT / 64];
   dsum_t* dsum = reinterpret_cast<dsum_t*>(lut2 + LUT2_N);       // [DSUM_N] direct series value sums
   const MetaLayout L = meta_layout(F);
   uint32_t* hdr = meta + L.hdr();
@@ -508,29 +509,17 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
         rcapv[j] = bcap[rb_bin];
       }
     }
-    if (wv == 0) {  // one wave: stage offsets and run ranks (DPP scans of 16 bins per lane), run heads
-      uint32_t c[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cnt + 16 * lane + 4 * q);
-        c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
-      }
-      uint32_t tl = 0, tr = 0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        tl += c[q];
-        tr += c[q] ? 1u : 0u;
-      }
-      uint32_t e = wave_incl_scan32(tl) - tl;
-      const uint32_t rin = wave_incl_scan32(tr);
-      uint32_t r = rin - tr;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        offr[16 * lane + q] = e | (r << 16);
-        if (c[q]) atomicOr(&heads[e >> 5], 1u << (e & 31u));
-        e += c[q];
-        r += c[q] ? 1u : 0u;
-      }
+    {  // stage offsets and run ranks: a block scan of {count, non-empty} (one bin per thread), run heads
+      static_assert(NT == BIN1_BINS && RB == 1, "one bin per thread");
+      const uint32_t pv = rn[0] | ((rn[0] ? 1u : 0u) << 16);  // (counts sum to <= CH < 2^16: no carry)
+      const uint32_t wi = wave_incl_scan32(pv);
+      if (lane == 63) wsum[wv] = wi;
+      __syncthreads();  // B1b: wave totals
+      uint32_t pre = 0;
+      for (int q = 0; q < wv; ++q) pre += wsum[q];
+      const uint32_t ex = pre + wi - pv;
+      offr[threadIdx.x] = ex;  // offset | run rank << 16
+      if (rn[0]) atomicOr(&heads[(ex & 0xFFFFu) >> 5], 1u << (ex & 31u));
     }
     uint32_t rec[PT];  // this thread's records, in slot order (read before any is scattered)
 #pragma unroll
@@ -587,7 +576,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     for (int k = 0; k < PT; ++k) {  // all CH entries, in sorted order (each wave a contiguous PT x 64 range)
       const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
       const uint32_t g = i >> 6;  // (wave-uniform)
-      const unsigned long long hw = ((unsigned long long)heads[2 * g + 1] << 32) | heads[2 * g];
+      const unsigned long long hw = *reinterpret_cast<const unsigned long long*>(heads + 2 * g);
       const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
       const uint32_t d = rdelta[run];
       if (d != NODEST) {

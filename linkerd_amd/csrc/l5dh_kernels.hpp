@@ -135,6 +135,8 @@ struct Plan {
   uint32_t* header;        // [4] cold items, big tiles, cold-item counter, split items; [4 + k B + b] per-workgroup
                            // sums of quantity k (B = ceil(F / 1024) plan workgroups); [4 + 4 B] split-item
                            // counter; [5 + 4 B] the unpacked encoding's words (sparse export)
+  uint32_t* big_hint;      // pinned, host-mapped word: this plan's big tiles (the host reads the last value
+                           // it sees only to pick the accumulate's launch order)
 };
 __host__ __device__ constexpr uint32_t plan_header_words(uint32_t F) { return 6 + 4 * ((F + 1023) / 1024); }
 // Sparse export (the fleet merge's reduce-scatter): words a tile's rows may take in the

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(1024) void k_plan_b(Segs segs, uint32_t F, int fina
         plan.header[3] = ty[2];
         plan.header[4 + 4 * B] = 0u;   // split-item counter
         plan.header[5 + 4 * B] = ty[3];  // the unpacked encoding's words
+        if (plan.big_hint) *reinterpret_cast<volatile uint32_t*>(plan.big_hint) = ty[1];
       }
     }
   }
@@ -341,6 +342,24 @@ __device__ __forceinline__ void count16(uint4 x, uint32_t m, Hist&& hist_add) {
   }
 }
 
+// count16 for the sparse export's clean items: the 8 returning adds go out together and
+// the first touches (a bin whose count was 0) are listed after them -- checked one by one
+// right after each add, every add waited for its return.
+template <class Hist, class Touch>
+__device__ __forceinline__ void count16_first(uint4 x, uint32_t m, Hist&& hist_add_rtn, Touch&& touched) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint32_t old[8], r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r[k] = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+    old[k] = 1u;
+    if ((uint32_t)k < m) old[k] = hist_add_rtn(r[k] >> 11, r[k] & 2047u);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if ((uint32_t)k < m && (((r[k] & 1u) ? old[k] >> 16 : old[k]) & 0xFFFFu) == 0u) touched(r[k] >> 11, r[k] & 2047u);
+}
+
 // The records of both halves of tile t in every segment: per segment, the two
 // ranges are walked together (a thread's loads of both halves in flight at once).
 // Ranges start 16-B aligned (rec16 regions at multiples of 8).
@@ -415,13 +434,13 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   uint32_t* tcnt = reinterpret_cast<uint32_t*>(midl + ROW);      // [2][HSER] (double-buffered by item parity)
   uint16_t* tlist = reinterpret_cast<uint16_t*>(tcnt + 2 * HSER);  // [HSER][ENC_LIST]
   int par = 0;
-  auto hist_add_enc = [&](uint32_t loc, uint32_t b) {
+  auto hist_add_rtn = [&](uint32_t loc, uint32_t b) -> uint32_t {
+    return atomicAdd(&hist[(loc & (HSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+  };
+  auto first_touch = [&](uint32_t loc, uint32_t b) {
     const uint32_t l = loc & (HSER - 1);
-    const uint32_t old = atomicAdd(&hist[l * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-    if ((((b & 1u) ? old >> 16 : old) & 0xFFFFu) == 0u) {
-      const uint32_t k = atomicAdd(&tcnt[par * HSER + l], 1u);
-      if (k < (uint32_t)ENC_LIST) tlist[l * ENC_LIST + k] = (uint16_t)b;
-    }
+    const uint32_t k = atomicAdd(&tcnt[par * HSER + l], 1u);
+    if (k < (uint32_t)ENC_LIST) tlist[l * ENC_LIST + k] = (uint16_t)b;
   };
   {
     uint4* p = reinterpret_cast<uint4*>(smem);
@@ -497,7 +516,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint32_t gn = g + NT;
         x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
         if (ENCODE && !dc)
-          count16(cx, min(8u, nc - 8 * g), hist_add_enc);
+          count16_first(cx, min(8u, nc - 8 * g), hist_add_rtn, first_touch);
         else
           count16(cx, min(8u, nc - 8 * g), hist_add);
       }
@@ -508,7 +527,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint4* p = reinterpret_cast<const uint4*>(r.r16 + r.a);
         for (uint32_t g = threadIdx.x; g < g0; g += NT) {
           if (ENCODE && !dc)
-            count16(p[g], min(8u, n - 8 * g), hist_add_enc);
+            count16_first(p[g], min(8u, n - 8 * g), hist_add_rtn, first_touch);
           else
             count16(p[g], min(8u, n - 8 * g), hist_add);
         }
@@ -620,17 +639,22 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         if (linear) {
           const int ng = lane_groups(lane);
           uint32_t g[9], nw = 0;
+          if (out.words) {  // (the merge encoding's words: the all-reduce export only)
 #pragma unroll
-          for (int q = 0; q < 9; ++q) {
-            g[q] = 0u;
-            if (q < ng) {
-              const uint4 v = SrcLds16{row}.get4(28 * lane + 4 * q);
-              g[q] = sum4(v);
-              nw += merge_words4(v);
+            for (int q = 0; q < 9; ++q) {
+              g[q] = 0u;
+              if (q < ng) {
+                const uint4 v = SrcLds16{row}.get4(28 * lane + 4 * q);
+                g[q] = sum4(v);
+                nw += merge_words4(v);
+              }
             }
+            put_words(nw, out.words + (s - out.first));
+          } else {
+#pragma unroll
+            for (int q = 0; q < 9; ++q) g[q] = q < ng ? SrcLds16{row}.sum4(28 * lane + 4 * q) : 0u;
           }
-          put_words(nw, out.words ? out.words + (s - out.first) : nullptr);
-          wave_summary(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
+          wave_summary<SrcLds16, true>(g, SrcLds16{row}, fixl[loc], midl, out.summ ? out.summ + (s - out.first) : nullptr);
           if (lane == 0 && out.totals) out.totals[s - out.first] = fixl[loc];
         } else {
           emit_series(SrcLds16{row}, s, 0, fixl[loc], dc, keep, final_mode, st, tbl, out);
