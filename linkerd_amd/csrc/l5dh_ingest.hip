@@ -301,7 +301,8 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // lut2 [1024] uint2, direct sums [255 x 32] u64.
 #ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
 __device__ unsigned long long g_phase1[1024 * 8];
-#define PH_INIT unsigned long long ph_acc[4] = {0, 0, 0, 0}, ph_t = wall_clock64();
+#define PH_INIT unsigned long long ph_acc[7] = {0, 0, 0, 0, 0, 0, 0}, ph_t = wall_clock64();
+#define PH_VWAIT asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #define PH_MARK(k)                                 \
   if (threadIdx.x == 0) {                          \
     const unsigned long long ph_n = wall_clock64(); \
@@ -310,12 +311,13 @@ __device__ unsigned long long g_phase1[1024 * 8];
   }
 #define PH_FLUSH                                                                   \
   if (threadIdx.x == 0 && pass == 0) {                                             \
-    for (int k = 0; k < 4; ++k) g_phase1[blockIdx.x * 8 + k] += ph_acc[k];          \
+    for (int k = 0; k < 7; ++k) g_phase1[blockIdx.x * 8 + k] += ph_acc[k];          \
     g_phase1[blockIdx.x * 8 + 7] += 1;                                             \
   }
 #else
 #define PH_INIT
 #define PH_MARK(k)
+#define PH_VWAIT
 #define PH_FLUSH
 #endif
 constexpr int CHW = 16384;
@@ -394,6 +396,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     const uint32_t cl = c0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      if (h == 1) { PH_MARK(1) }
       uint32_t sv[PH];
       float fv[PH];
       if (full) {
@@ -423,6 +426,10 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
           fv[k] = in ? values[i] : 0.0f;
           bad |= in && sv[k] >= S;
         }
+      }
+      if (full) {  // (phase stamps: the half's loads -- and, on gfx9, every older store -- done)
+        PH_VWAIT
+        if (h == 0) { PH_MARK(0) } else { PH_MARK(2) }
       }
 #pragma unroll
       for (int g = 0; g < PH; g += GS) {
@@ -494,7 +501,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B1: counts complete
-    PH_MARK(0)
+    PH_MARK(3)
     // run reservations: thread t -> bins t, t + NT, ... (the trash bin TB gets none)
     constexpr int RB = (BIN1_BINS + NT - 1) / NT;
     uint32_t rn[RB], rold[RB], rbase[RB], rcapv[RB];
@@ -528,7 +535,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       rec[4 * kk] = v.x; rec[4 * kk + 1] = v.y; rec[4 * kk + 2] = v.z; rec[4 * kk + 3] = v.w;
     }
     __syncthreads();  // B2: offsets, run ranks, heads; every slot-order record read
-    PH_MARK(1)
+    PH_MARK(4)
     // (after B2: the run reservations' returns and the scan never wait behind these loads)
     if (vec && c0 + 2u * (uint32_t)CH <= hi) prefetch(c0 + (uint32_t)CH);
 #pragma unroll
@@ -567,7 +574,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B3: stage, group prefixes, deltas (every count read: cleared below)
-    PH_MARK(2)
+    PH_MARK(5)
     const uint32_t nst = offr[FS] >> 16;  // runs of super-tile bins (u32 records); the later runs are u16
 #pragma unroll
     for (int j = 0; j < RB; ++j)
@@ -587,7 +594,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
     }
     __syncthreads();  // B4
-    PH_MARK(3)
+    PH_MARK(6)
   }
   PH_FLUSH
   if (pass == 0) {

@@ -342,24 +342,6 @@ __device__ __forceinline__ void count16(uint4 x, uint32_t m, Hist&& hist_add) {
   }
 }
 
-// count16 for the sparse export's clean items: the 8 returning adds go out together and
-// the first touches (a bin whose count was 0) are listed after them -- checked one by one
-// right after each add, every add waited for its return.
-template <class Hist, class Touch>
-__device__ __forceinline__ void count16_first(uint4 x, uint32_t m, Hist&& hist_add_rtn, Touch&& touched) {
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-  uint32_t old[8], r[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    r[k] = (w[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-    old[k] = 1u;
-    if ((uint32_t)k < m) old[k] = hist_add_rtn(r[k] >> 11, r[k] & 2047u);
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    if ((uint32_t)k < m && (((r[k] & 1u) ? old[k] >> 16 : old[k]) & 0xFFFFu) == 0u) touched(r[k] >> 11, r[k] & 2047u);
-}
-
 // The records of both halves of tile t in every segment: per segment, the two
 // ranges are walked together (a thread's loads of both halves in flight at once).
 // Ranges start 16-B aligned (rec16 regions at multiples of 8).
@@ -434,13 +416,15 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
   uint32_t* tcnt = reinterpret_cast<uint32_t*>(midl + ROW);      // [2][HSER] (double-buffered by item parity)
   uint16_t* tlist = reinterpret_cast<uint16_t*>(tcnt + 2 * HSER);  // [HSER][ENC_LIST]
   int par = 0;
-  auto hist_add_rtn = [&](uint32_t loc, uint32_t b) -> uint32_t {
-    return atomicAdd(&hist[(loc & (HSER - 1)) * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
-  };
-  auto first_touch = [&](uint32_t loc, uint32_t b) {
+  // (batching the 8 adds of a group and listing the first touches after them measured
+  // +0.02 ms per C4 rank, round 5)
+  auto hist_add_enc = [&](uint32_t loc, uint32_t b) {
     const uint32_t l = loc & (HSER - 1);
-    const uint32_t k = atomicAdd(&tcnt[par * HSER + l], 1u);
-    if (k < (uint32_t)ENC_LIST) tlist[l * ENC_LIST + k] = (uint16_t)b;
+    const uint32_t old = atomicAdd(&hist[l * CROW + (b >> 1)], (b & 1u) ? 0x10000u : 1u);
+    if ((((b & 1u) ? old >> 16 : old) & 0xFFFFu) == 0u) {
+      const uint32_t k = atomicAdd(&tcnt[par * HSER + l], 1u);
+      if (k < (uint32_t)ENC_LIST) tlist[l * ENC_LIST + k] = (uint16_t)b;
+    }
   };
   {
     uint4* p = reinterpret_cast<uint4*>(smem);
@@ -516,7 +500,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint32_t gn = g + NT;
         x = gn < g0 ? p0[gn] : make_uint4(0u, 0u, 0u, 0u);
         if (ENCODE && !dc)
-          count16_first(cx, min(8u, nc - 8 * g), hist_add_rtn, first_touch);
+          count16(cx, min(8u, nc - 8 * g), hist_add_enc);
         else
           count16(cx, min(8u, nc - 8 * g), hist_add);
       }
@@ -527,7 +511,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint4* p = reinterpret_cast<const uint4*>(r.r16 + r.a);
         for (uint32_t g = threadIdx.x; g < g0; g += NT) {
           if (ENCODE && !dc)
-            count16_first(p[g], min(8u, n - 8 * g), hist_add_rtn, first_touch);
+            count16(p[g], min(8u, n - 8 * g), hist_add_enc);
           else
             count16(p[g], min(8u, n - 8 * g), hist_add);
         }

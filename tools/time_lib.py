@@ -62,7 +62,8 @@ def main():
         if not act:
             continue
         # wall_clock64 runs at 100 MHz: ticks * 0.01 us; per launch, averaged over workgroups
-        per = [sum(x[k] for x in act) / sum(x[7] for x in act) * 0.01 for k in range(4)]
+        per = [sum(x[k] for x in act) / sum(x[7] for x in act) * 0.01 for k in range(7)]
+        per = [v for v in per if v > 0] if name == "cold" else per
         print(f"  phases {name} ({len(act)} wgs, us per launch per wg): " +
               " ".join(f"p{k}={v:.1f}" for k, v in enumerate(per)), flush=True)
 
