@@ -301,6 +301,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
 // lut2 [1024] uint2, direct sums [255 x 32] u64.
 #ifdef L5DH_PHASES  // development (tools/mk_var.sh, tools/time_lib.py): per-workgroup phase times
 __device__ unsigned long long g_phase1[1024 * 8];
+__device__ unsigned long long g_phase3[1024 * 8];  // level 2
 #define PH_INIT unsigned long long ph_acc[7] = {0, 0, 0, 0, 0, 0, 0}, ph_t = wall_clock64();
 #define PH_VWAIT asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #define PH_MARK(k)                                 \
@@ -854,6 +855,17 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   uint4 x[PG];
   load(a, e, x);
   uint32_t prev_total = 0;
+#ifdef L5DH_PHASES
+  unsigned long long ph2[5] = {0, 0, 0, 0, 0}, ph2_t = wall_clock64();
+#define PH2_MARK(k)                                  \
+  if (threadIdx.x == 0) {                            \
+    const unsigned long long ph_n = wall_clock64();  \
+    ph2[k] += ph_n - ph2_t;                          \
+    ph2_t = ph_n;                                    \
+  }
+#else
+#define PH2_MARK(k)
+#endif
   for (uint32_t item = i0; item < i1; ++item) {
     const int b = (int)(item & 1u);
     const uint32_t cj = j, ctot = e - a;
@@ -904,6 +916,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       }
     }
     __syncthreads();  // B1: counts complete
+    PH2_MARK(0)
     // (C) run reservations (waves 0 and 1, lane = key; results read in (F)); wave 2
     // scans the counts into this item's stage offsets
     uint32_t rc = 0, rold = 0, rbase = 0, rcapv = 0;
@@ -923,6 +936,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       ocx[b * B2_KEYS + 2 * lane + 1].x = ex + c0;
     }
     __syncthreads();  // B2: stage offsets visible; every count read
+    PH2_MARK(1)
     // (D) scatter this item into its stage
     {
       uint32_t* st = stage + b * ITEM2;
@@ -940,8 +954,10 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
           if (kr[k0 + j] != NOKEY) st[o[j] + rank[k0 + j]] = kr[k0 + j];
       }
     }
+    PH2_MARK(2)
     // (E) write-out of the previous item (its stage and run offsets are complete)
     if (item > i0) write_out(b ^ 1, prev_total);
+    PH2_MARK(3)
     // (F) this item's run bases; counts cleared for the next item
     if (wv < 2) {
       uint32_t rb = INVALID;
@@ -953,6 +969,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       cnt[rk] = 0u;
     }
     __syncthreads();  // B3
+    PH2_MARK(4)
     prev_total = ctot;
 #pragma unroll
     for (int g = 0; g < PG; ++g) x[g] = xn[g];
@@ -960,6 +977,12 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   write_out((int)((i1 - 1) & 1u), prev_total);
   __syncthreads();
   if (pass == 0) flush(cur_j);
+#ifdef L5DH_PHASES
+  if (threadIdx.x == 0 && pass == 0) {
+    for (int k = 0; k < 5; ++k) g_phase3[blockIdx.x * 8 + k] += ph2[k];
+    g_phase3[blockIdx.x * 8 + 7] += 1;
+  }
+#endif
 }
 
 // After level 2, over the key workgroups: k_rfix2a copies the exact key counts to
@@ -1027,6 +1050,9 @@ __global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__
 }  // namespace
 
 #ifdef L5DH_PHASES
+extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases3(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase3), sizeof(g_phase3), 0, hipMemcpyDeviceToHost);
+}
 extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases1(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase1), sizeof(g_phase1), 0, hipMemcpyDeviceToHost);
 }

@@ -44,7 +44,7 @@ def main():
     eng.set_param(N.PARAM_TIMING, 1)
     eng.kernel_times(reset=True)
     core = N.load()
-    phases = [getattr(core, f"l5dh_dev_phases{i}", None) for i in (1, 2)]  # (L5DH_PHASES builds)
+    phases = [getattr(core, f"l5dh_dev_phases{i}", None) for i in (1, 2, 3)]  # (L5DH_PHASES builds)
     before = [snap_phases(f) for f in phases]
     for k in range(steps):
         eng.ingest(*batches[k % 2])
@@ -53,7 +53,7 @@ def main():
     tot = sum(ms for ms, n in kt.values() if n) / steps
     print(f"{os.path.basename(N.LIB_PATH)}: {tot:.4f} ms/step  " +
           "  ".join(f"{k} {ms / steps:.4f}" for k, (ms, n) in kt.items() if n), flush=True)
-    for name, f, b in zip(("level1", "cold"), phases, before):
+    for name, f, b in zip(("level1", "cold", "level2"), phases, before):
         if f is None:
             continue
         a = snap_phases(f)
@@ -63,7 +63,7 @@ def main():
             continue
         # wall_clock64 runs at 100 MHz: ticks * 0.01 us; per launch, averaged over workgroups
         per = [sum(x[k] for x in act) / sum(x[7] for x in act) * 0.01 for k in range(7)]
-        per = [v for v in per if v > 0] if name == "cold" else per
+        per = [v for v in per if v > 0] if name != "level1" else per
         print(f"  phases {name} ({len(act)} wgs, us per launch per wg): " +
               " ".join(f"p{k}={v:.1f}" for k, v in enumerate(per)), flush=True)
 
