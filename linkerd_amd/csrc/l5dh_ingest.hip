@@ -395,6 +395,19 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
     const uint32_t cl = c0;
+#ifdef L5DH_EARLY
+    uint4 hs[PH / 4], hv[PH / 4];  // the second half, issued during the first's ranking
+    auto load_second = [&]() {
+      if (full) {
+#pragma unroll
+        for (int k = 0; k < PH / 4; ++k) {
+          const uint32_t base = cl + 4u * ((uint32_t)(PH / 4 + k) * NT + threadIdx.x);
+          hs[k] = *reinterpret_cast<const uint4*>(series + base);
+          hv[k] = *reinterpret_cast<const uint4*>(values + base);
+        }
+      }
+    };
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1) { PH_MARK(1) }
@@ -410,8 +423,13 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
             u4 = pfv[h * (PH / 4) + k];
           } else {  // (issued here: in flight during the first half's ranking, they spill registers;
                     // a timing-only build that skips them saved 0.1 ms of bin1, round 5)
+#ifdef L5DH_EARLY
+            s4 = hs[k];
+            u4 = hv[k];
+#else
             s4 = *reinterpret_cast<const uint4*>(series + base);
             u4 = *reinterpret_cast<const uint4*>(values + base);
+#endif
           }
           const float4 f4 = make_float4(__uint_as_float(u4.x), __uint_as_float(u4.y), __uint_as_float(u4.z),
                                         __uint_as_float(u4.w));
@@ -434,6 +452,9 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
 #pragma unroll
       for (int g = 0; g < PH; g += GS) {
+#ifdef L5DH_EARLY
+        if (h == 0 && g == L5DH_EARLY * GS) load_second();
+#endif
         uint32_t pl[GS];
         uint32_t escm = 0;
 #pragma unroll
@@ -462,18 +483,14 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
             }
           }
         }
-        // (The LUT read and the value-sum atomic are branches around the direct slots:
-        // an unconditional, branch-free version -- every slot reading the LUT and adding
-        // 0 to a spare sum -- was slower, bin1 3.89 -> 3.96 ms, profiles/r04i_ab.txt.)
         uint2 dv[GS], lv[GS];
 #pragma unroll
         for (int q = 0; q < GS; ++q) dv[q] = dw[(sv[g + q] >> (TILE_SHIFT + 5)) & 1023u];  // (any word when s >= S)
 #pragma unroll
-        for (int q = 0; q < GS; ++q) {  // the bucket LUT, read by the direct slots only
-          lv[q] = make_uint2(0u, 0u);
-          if (__builtin_amdgcn_ubfe(dv[q].x, __builtin_amdgcn_ubfe(sv[g + q], TILE_SHIFT, 5), 1) != 0u)
-            lv[q] = lut2[lut2_index(pl[q])];
-        }
+        // the bucket LUT, read by every slot: issued with the dw reads instead of behind them
+        // (only a direct slot uses it; reading it under the direct bit waited for dw first:
+        // bin1 3.31 -> 3.25 ms on C3, C2 unchanged, round 5)
+        for (int q = 0; q < GS; ++q) lv[q] = lut2[lut2_index(pl[q])];
         uint32_t rc4[GS];
 #pragma unroll
         for (int q = 0; q < GS; ++q) {

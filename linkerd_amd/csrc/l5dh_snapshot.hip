@@ -616,6 +616,7 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         for (int i = lane; i < CROW / 4; i += 64) hr[i] = make_uint4(0u, 0u, 0u, 0u);
       }
     }
+    // (two series' summaries interleaved per wave, unrolled: accumulate +0.02 ms, round 5)
     for (int loc = w; !ENCODE && loc < HSER; loc += NT / 64) {
       const uint32_t s = s0 + loc;
       const uint32_t* row = hist + loc * CROW;
