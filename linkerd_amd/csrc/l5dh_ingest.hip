@@ -321,6 +321,15 @@ __device__ unsigned long long g_phase3[1024 * 8];  // level 2
 #define PH_VWAIT
 #define PH_FLUSH
 #endif
+#ifdef L5DH_NTL
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) {  // the batch: read once
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+#else
+__device__ __forceinline__ uint4 ld_stream(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+#endif
 constexpr int CHW = 16384;
 using dsum_t = unsigned long long;
 // rdelta of a dropped run: a valid delta (run base - stage offset) lies in (-CHW, cap16),
@@ -383,8 +392,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
 #pragma unroll
     for (int k = 0; k < PFG; ++k) {
       const uint32_t base = c + 4u * ((uint32_t)k * NT + threadIdx.x);
-      pfs[k] = *reinterpret_cast<const uint4*>(series + base);
-      pfv[k] = *reinterpret_cast<const uint4*>(values + base);
+      pfs[k] = ld_stream(series + base);
+      pfv[k] = ld_stream(reinterpret_cast<const uint32_t*>(values) + base);
     }
   };
   if (vec && lo + (uint32_t)CH <= hi) prefetch(lo);
@@ -395,19 +404,20 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     uint32_t pk[PT];  // [14:0] rank | [24:15] bin
     const bool full = vec && c0 + (uint32_t)CH <= hi;
     const uint32_t cl = c0;
-#ifdef L5DH_EARLY
-    uint4 hs[PH / 4], hv[PH / 4];  // the second half, issued during the first's ranking
+    // the second half, issued once the first half's first group is ranked (in flight through
+    // the rest of its ranking): bin1 3.25-3.30 -> 3.18 ms on C3 (issued before the first group,
+    // or at the second half's start as in round 4, 3.36 / 3.25; profiles/r05w_second_half_ab.txt)
+    uint4 hs[PH / 4], hv[PH / 4];
     auto load_second = [&]() {
       if (full) {
 #pragma unroll
         for (int k = 0; k < PH / 4; ++k) {
           const uint32_t base = cl + 4u * ((uint32_t)(PH / 4 + k) * NT + threadIdx.x);
-          hs[k] = *reinterpret_cast<const uint4*>(series + base);
-          hv[k] = *reinterpret_cast<const uint4*>(values + base);
+          hs[k] = ld_stream(series + base);
+          hv[k] = ld_stream(reinterpret_cast<const uint32_t*>(values) + base);
         }
       }
     };
-#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1) { PH_MARK(1) }
@@ -416,20 +426,13 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       if (full) {
 #pragma unroll
         for (int k = 0; k < PH / 4; ++k) {
-          const uint32_t base = cl + 4u * ((uint32_t)(h * (PH / 4) + k) * NT + threadIdx.x);
           uint4 s4, u4;
           if (h == 0) {
             s4 = pfs[h * (PH / 4) + k];
             u4 = pfv[h * (PH / 4) + k];
-          } else {  // (issued here: in flight during the first half's ranking, they spill registers;
-                    // a timing-only build that skips them saved 0.1 ms of bin1, round 5)
-#ifdef L5DH_EARLY
+          } else {
             s4 = hs[k];
             u4 = hv[k];
-#else
-            s4 = *reinterpret_cast<const uint4*>(series + base);
-            u4 = *reinterpret_cast<const uint4*>(values + base);
-#endif
           }
           const float4 f4 = make_float4(__uint_as_float(u4.x), __uint_as_float(u4.y), __uint_as_float(u4.z),
                                         __uint_as_float(u4.w));
@@ -452,9 +455,7 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       }
 #pragma unroll
       for (int g = 0; g < PH; g += GS) {
-#ifdef L5DH_EARLY
-        if (h == 0 && g == L5DH_EARLY * GS) load_second();
-#endif
+        if (h == 0 && g == GS) load_second();
         uint32_t pl[GS];
         uint32_t escm = 0;
 #pragma unroll
@@ -606,9 +607,17 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const uint32_t d = rdelta[run];
       if (d != NODEST) {
         if (run < nst)
+#ifdef L5DH_NT1
+          __builtin_nontemporal_store(stage[i], rec32 + i + d);
+#else
           rec32[i + d] = stage[i];
+#endif
         else
+#ifdef L5DH_NT1
+          __builtin_nontemporal_store((uint16_t)stage[i], rec16 + i + d);
+#else
           rec16[i + d] = (uint16_t)stage[i];
+#endif
       }
     }
     __syncthreads();  // B4

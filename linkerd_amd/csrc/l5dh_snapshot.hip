@@ -663,7 +663,13 @@ __global__ __launch_bounds__(512, 2) void k_accum_cold_h(Segs segs, Plan plan, S
         const uint32_t x = *p0, y = *p1;
         *p0 = 0u;
         *p1 = 0u;
+#ifdef L5DH_NTC
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v4 = {x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16};
+        __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(o + c));
+#else
         o[c] = make_uint4(x & 0xFFFFu, x >> 16, y & 0xFFFFu, y >> 16);
+#endif
       }
     }
     if (threadIdx.x == 0) {
