@@ -6,7 +6,7 @@
 //   k_rplan1   this batch's direct tiles (the biggest estimated) and the level-1 bin
 //              regions (super-tiles; two half-bins per direct tile), sized from the
 //              previous batch's exact key counts and this batch's sample
-//   k_rbin1w   level 1: LDS counting sort of 24K-sample sub-chunks by bin; each run's
+//   k_rbin1w   level 1: LDS counting sort of 16K-sample sub-chunks by bin; each run's
 //              place in its bin's region comes from ONE returning global atomic per
 //              (sub-chunk, bin) on the bin's cursor (order inside a region is free:
 //              integer sums do not depend on it); direct tiles' samples bucketized
@@ -15,7 +15,7 @@
 //              and a second k_rbin1w pass (launched always, it exits unless needed);
 //              the direct keys' ranges; the invalid-id count to the host
 //   k_rplan2a/b level-2 regions of the other keys (with the level-1 plan; k_rfix1
-//              plans the level-2 items: 16K records of a super-tile's level-1 region)
+//              plans the level-2 items: 6K records of a super-tile's level-1 region)
 //   k_rbin2    level 2: an item LDS-sorted by key into 16-bit records (series in
 //              tile | bucket) in its keys' regions; value sums folded into sumfix
 //   k_rfix2a/b exact key counts -> kprev (the next batch's prediction); overflow ->
@@ -845,16 +845,20 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   auto write_out = [&](int bb, uint32_t total) {
     const uint32_t* st = stage + bb * ITEM2;
     const uint2* oc = ocx + bb * B2_KEYS;
+#ifndef L5DH_B2W
+#define L5DH_B2W 4
+#endif
+    constexpr int WB = L5DH_B2W;
 #pragma unroll
-    for (int k0 = 0; k0 < PT; k0 += 4) {
-      uint32_t x[4];
-      uint2 o[4];
+    for (int k0 = 0; k0 < PT; k0 += WB) {
+      uint32_t x[WB];
+      uint2 o[WB];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = st[(uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane];
+      for (int j = 0; j < WB; ++j) x[j] = st[(uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = oc[(x[j] >> 16) & (B2_KEYS - 1)];
+      for (int j = 0; j < WB; ++j) o[j] = oc[(x[j] >> 16) & (B2_KEYS - 1)];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < WB; ++j) {
         const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)(k0 + j) * 64 + (uint32_t)lane;
         if (i < total && o[j].y != INVALID) rec16[o[j].y + (i - o[j].x)] = (uint16_t)(x[j] & 0xFFFFu);
       }
@@ -906,7 +910,10 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       // when it has nothing to add), so the atomics of consecutive slots stay in flight
       // together.  The branchy form (rank = valid ? atomicAdd : 0, sum under an if) had an
       // lgkmcnt(0) wait behind every rank atomic (round 5).
-      constexpr int H = PT / 2;  // LUT reads batched per half (bounded register pressure)
+#ifndef L5DH_B2H
+#define L5DH_B2H 2
+#endif
+      constexpr int H = PT / L5DH_B2H;  // LUT reads batched per half (bounded register pressure)
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
         uint2 lv[H];
@@ -956,12 +963,12 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       // read of ocx above a store to the stage, so a read-store pair per slot waited on
       // every read)
 #pragma unroll
-      for (int k0 = 0; k0 < PT; k0 += 4) {
-        uint32_t o[4];
+      for (int k0 = 0; k0 < PT; k0 += L5DH_B2W) {
+        uint32_t o[L5DH_B2W];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
+        for (int j = 0; j < L5DH_B2W; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < L5DH_B2W; ++j)
           if (kr[k0 + j] != NOKEY) st[o[j] + rank[k0 + j]] = kr[k0 + j];
       }
     }
