@@ -367,7 +367,6 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t TB = FS + 2 * ND;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  const unsigned long long mle = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
   for (uint32_t w = threadIdx.x; w < NW; w += NT) dw[w] = make_uint2(meta[L.dbits() + w], meta[L.dpre() + w]);
   for (uint32_t b = threadIdx.x; b < BIN1_BINS; b += NT) cnt[b] = 0;
   for (uint32_t i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
@@ -377,6 +376,15 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   const uint32_t lo = (uint32_t)((size_t)blockIdx.x * per);
   const uint32_t hi = (uint32_t)min((size_t)lo + per, n);
   bool bad = false;
+  // this thread's bins' regions (fixed for the launch): loaded once, not per sub-chunk
+  constexpr int RB0 = (BIN1_BINS + NT - 1) / NT;
+  uint32_t my_base[RB0], my_cap[RB0];
+#pragma unroll
+  for (int j = 0; j < RB0; ++j) {
+    const uint32_t b = threadIdx.x + (uint32_t)j * NT;
+    my_base[j] = b < TB ? bbase[b] : 0u;
+    my_cap[j] = b < TB ? bcap[b] : 0u;
+  }
   PH_INIT
   // the next sub-chunk's first half loaded during this one's scatter / write-out
   constexpr int PFG = PH / 4;  // prefetched 16-B groups per array
@@ -521,12 +529,10 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
     for (int j = 0; j < RB; ++j) {
       const uint32_t rb_bin = threadIdx.x + (uint32_t)j * NT;
       rn[j] = rb_bin <= TB ? cnt[rb_bin] : 0u;  // records of the bin in this sub-chunk
-      rold[j] = rbase[j] = rcapv[j] = 0;
-      if (rb_bin < TB && rn[j]) {
-        rold[j] = atomicAdd(&bcnt[rb_bin], rn[j]);
-        rbase[j] = bbase[rb_bin];
-        rcapv[j] = bcap[rb_bin];
-      }
+      rold[j] = 0;
+      rbase[j] = my_base[j];
+      rcapv[j] = my_cap[j];
+      if (rb_bin < TB && rn[j]) rold[j] = atomicAdd(&bcnt[rb_bin], rn[j]);
     }
     {  // stage offsets and run ranks: a block scan of {count, non-empty} (one bin per thread), run heads
       static_assert(NT == BIN1_BINS && RB == 1, "one bin per thread");
@@ -596,7 +602,8 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
       const uint32_t i = (uint32_t)wv * (PT * 64) + (uint32_t)k * 64 + (uint32_t)lane;
       const uint32_t g = i >> 6;  // (wave-uniform)
       const unsigned long long hw = *reinterpret_cast<const unsigned long long*>(heads + 2 * g);
-      const uint32_t run = (uint32_t)gpre[g] + (uint32_t)__popcll(hw & mle) - 1u;
+      // run heads at or before this lane: those below it (mbcnt) + its own bit
+      const uint32_t run = (uint32_t)gpre[g] + mask_below(hw) + (uint32_t)((hw >> lane) & 1ull) - 1u;
       const uint32_t d = rdelta[run];
       if (d != NODEST) {
         if (run < nst)
@@ -845,10 +852,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   auto write_out = [&](int bb, uint32_t total) {
     const uint32_t* st = stage + bb * ITEM2;
     const uint2* oc = ocx + bb * B2_KEYS;
-#ifndef L5DH_B2W
-#define L5DH_B2W 4
-#endif
-    constexpr int WB = L5DH_B2W;
+    constexpr int WB = 4;
 #pragma unroll
     for (int k0 = 0; k0 < PT; k0 += WB) {
       uint32_t x[WB];
@@ -910,10 +914,9 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       // when it has nothing to add), so the atomics of consecutive slots stay in flight
       // together.  The branchy form (rank = valid ? atomicAdd : 0, sum under an if) had an
       // lgkmcnt(0) wait behind every rank atomic (round 5).
-#ifndef L5DH_B2H
-#define L5DH_B2H 2
-#endif
-      constexpr int H = PT / L5DH_B2H;  // LUT reads batched per half (bounded register pressure)
+      // LUT reads batched per half (all 12 at once, or the scatter / write-out batches of 12
+      // instead of 4: level 2 +0.01..+0.03 ms, round 5)
+      constexpr int H = PT / 2;
 #pragma unroll
       for (int k = 0; k < PT; ++k) {
         uint2 lv[H];
@@ -963,12 +966,12 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       // read of ocx above a store to the stage, so a read-store pair per slot waited on
       // every read)
 #pragma unroll
-      for (int k0 = 0; k0 < PT; k0 += L5DH_B2W) {
-        uint32_t o[L5DH_B2W];
+      for (int k0 = 0; k0 < PT; k0 += 4) {
+        uint32_t o[4];
 #pragma unroll
-        for (int j = 0; j < L5DH_B2W; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
+        for (int j = 0; j < 4; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
 #pragma unroll
-        for (int j = 0; j < L5DH_B2W; ++j)
+        for (int j = 0; j < 4; ++j)
           if (kr[k0 + j] != NOKEY) st[o[j] + rank[k0 + j]] = kr[k0 + j];
       }
     }
