@@ -72,10 +72,10 @@ METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # measured single-GPU steps; the plan is derived from per-tile loads
 # (fleet.plan_shards) -- here the workload's expected load, in a fleet the previous
 # interval's l5dh_tile_totals
-# fleet.CostModel fitted by tools/fit_cost.py to the two round-4 8-way shard sweeps + the C3/C2/C1
-# lines (profiles/r04_shard_sweeps_joint_fit.txt: 19 lines, every one within 4.2 %)
-C3_COST = dict(per_sample=4.05e-9, per_series=1.36e-6, per_sample_fold=2.59e-9, fixed=0.242, per_sample_l2=2.47e-9,
-               per_sample_hot=7.37e-11, fixed_fold=0.0513)
+# fleet.CostModel fitted by tools/fit_cost.py to the round-5 8-way shard sweep + the C3/C2/C1
+# lines at the same sources (profiles/r05_shard_sweep_fit.txt: 11 lines, every one within 3.1 %)
+C3_COST = dict(per_sample=3.11e-09, per_series=1.13e-06, per_sample_fold=2.55e-09, fixed=0.168,
+               per_sample_l2=2.51e-09, per_sample_hot=5.3e-10, fixed_fold=0.0368)
 
 
 def parse():
