@@ -65,7 +65,8 @@ KERNEL_ALG_BYTES = {
 # the engine's timed phases (l5dh_kernel_time ids) -> the default build's kernels in the PMC
 # summary whose per-launch bytes add up to the phase (the two accumulate kernels run
 # side by side: one launch of each per snapshot)
-PMC_KERNELS = {"bin1": ["rbin1w"], "bin2": ["rbin2"], "accum": ["accum_cold_h", "accum_split"]}
+# (the accumulate phase's timer spans k_hot_finish too: it runs under the cold kernel)
+PMC_KERNELS = {"bin1": ["rbin1w"], "bin2": ["rbin2"], "accum": ["accum_cold_h", "accum_split", "hot_finish"]}
 METRIC = "histogram samples ingested+summarized/sec (1M series) and % HBM peak"
 # device cost model of one step on MI355X for the C3 shard plan (fleet.CostModel): one
 # per-sample, per-series and fold cost for any series / sample count, fitted to the

@@ -1129,15 +1129,18 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 }
 
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
-                              Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st) {
+                              Outputs out, int direct_out, uint32_t hot_chunk, bool beside_cold, hipStream_t st) {
   if (max_split_items == 0) return hipSuccess;
-  // at most 3/8 of the CUs: launched before the cold tiles' kernel, it leaves the rest to
-  // it (k_accum_split takes 115 KB of LDS: the two cannot share a CU), and its workgroups
-  // and the cold ones take items until both queues are empty (accumulate phase on C3:
-  // 1.67 ms with every CU first, 1.63 with half, 1.61 with 3/8; 1/4: 1.85, 5/8: 1.65;
-  // profiles/r05ab_split_fraction_ab.txt)
-  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, (uint32_t)num_cus() * 3 / 8)), dim3(WG),
-                     ACC_SPLIT_LDS, st, segs, plan, state, tb, out, direct_out, hot_chunk);
+  // beside the cold tiles' kernel (on the side stream) at most 3/8 of the CUs: launched
+  // first, it leaves the rest to it (k_accum_split takes 115 KB of LDS: the two cannot
+  // share a CU), and its workgroups and the cold ones take items until both queues are
+  // empty (accumulate phase on C3: 1.67 ms with every CU first, 1.63 with half, 1.61 with
+  // 3/8; 1/4: 1.85, 5/8: 1.65; profiles/r05ab_split_fraction_ab.txt).  Alone on its stream
+  // (the cold kernel queued after it) it takes every CU.
+  const uint32_t cus = (uint32_t)num_cus();
+  const uint32_t g = std::max<uint32_t>(1u, beside_cold ? cus * 3 / 8 : cus);
+  hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, g)), dim3(WG), ACC_SPLIT_LDS, st, segs,
+                     plan, state, tb, out, direct_out, hot_chunk);
   return hipGetLastError();
 }
 

@@ -290,6 +290,47 @@ int l5do_ingest(l5do_hist* hists, size_t nseries, const uint32_t* series,
   return bad ? -2 : 0;
 }
 
+typedef struct {
+  const int32_t* counts;
+  const int64_t* totals;
+  l5do_summary* out;
+  size_t lo, hi;
+} summary_job;
+
+static void* summary_worker(void* arg) {
+  summary_job* j = (summary_job*)arg;
+  for (size_t s = j->lo; s < j->hi; s++)
+    l5do_summary_of_counts(j->counts + s * L5DO_NBUCKETS, j->totals[s], &j->out[s]);
+  return NULL;
+}
+
+/* Metric.scala:53-67 for n dense rows (each row independent: split over `threads`). */
+int l5do_summarize_counts_n(const int32_t* counts, const int64_t* totals, size_t n, l5do_summary* out,
+                            int threads) {
+  if (threads < 1) threads = 1;
+  if ((size_t)threads > n) threads = n ? (int)n : 1;
+  pthread_t* tids = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  summary_job* jobs = (summary_job*)malloc(sizeof(summary_job) * threads);
+  if (!tids || !jobs) {
+    free(tids);
+    free(jobs);
+    return -3;
+  }
+  size_t per = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    jobs[t].counts = counts;
+    jobs[t].totals = totals;
+    jobs[t].out = out;
+    jobs[t].lo = (size_t)t * per < n ? (size_t)t * per : n;
+    jobs[t].hi = jobs[t].lo + per < n ? jobs[t].lo + per : n;
+    pthread_create(&tids[t], NULL, summary_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(tids[t], NULL);
+  free(tids);
+  free(jobs);
+  return 0;
+}
+
 /* AdminMetricsExportTelemeter.scala:154-162: for each Stat, snapshot() then reset() */
 void l5do_snapshot_all(l5do_hist* hists, size_t nseries, l5do_summary* out, int reset) {
   for (size_t s = 0; s < nseries; s++) {

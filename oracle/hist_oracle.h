@@ -83,6 +83,10 @@ int l5do_ingest(l5do_hist* hists, size_t nseries, const uint32_t* series,
 /* Snapshot every series single-threaded (the DefaultTimer thread,
  * AdminMetricsExportTelemeter.scala:154-162): summary then optional reset. */
 void l5do_snapshot_all(l5do_hist* hists, size_t nseries, l5do_summary* out, int reset);
+/* Summaries of n dense int32 count rows + int64 totals (l5do_summary_of_counts per
+ * row), rows split over `threads` workers.  Returns 0, or -3 on allocation failure. */
+int l5do_summarize_counts_n(const int32_t* counts, const int64_t* totals, size_t n, l5do_summary* out,
+                            int threads);
 /* Copy dense counts/totals out. */
 void l5do_export(const l5do_hist* hists, size_t nseries, int32_t* counts, int64_t* totals);
 size_t l5do_hist_size(void);

@@ -85,6 +85,9 @@ def lib():
             L.l5do_snapshot_all.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
             L.l5do_summary_of_counts.restype = None
             L.l5do_summary_of_counts.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+            L.l5do_summarize_counts_n.restype = ctypes.c_int
+            L.l5do_summarize_counts_n.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.c_void_p, ctypes.c_int]
             L.l5do_export.restype = None
             L.l5do_export.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
             L.l5do_hist_size.restype = ctypes.c_size_t
@@ -126,14 +129,16 @@ class OracleHistograms:
         return self.h["num"].copy()
 
 
-def summarize_counts(counts: np.ndarray, totals: np.ndarray) -> np.ndarray:
-    """Summaries for dense int32 count rows + int64 totals (num = sum of counts)."""
+def summarize_counts(counts: np.ndarray, totals: np.ndarray, threads: int = 1) -> np.ndarray:
+    """Summaries for dense int32 count rows + int64 totals (num = sum of counts):
+    l5do_summary_of_counts per row, rows split over `threads` workers (one C call)."""
     counts = np.ascontiguousarray(counts, dtype=np.int32).reshape(-1, NBUCKETS)
     totals = np.ascontiguousarray(totals, dtype=np.int64).reshape(-1)
+    assert totals.shape[0] == counts.shape[0]
     out = np.zeros(counts.shape[0], dtype=SUMMARY_DTYPE)
-    L = lib()
-    for i in range(counts.shape[0]):
-        L.l5do_summary_of_counts(counts[i].ctypes.data, int(totals[i]), out[i:i + 1].ctypes.data)
+    rc = lib().l5do_summarize_counts_n(counts.ctypes.data, totals.ctypes.data, counts.shape[0],
+                                       out.ctypes.data, int(threads))
+    assert rc == 0, f"l5do_summarize_counts_n: {rc}"
     return out
 
 

@@ -140,7 +140,7 @@ def test_pmc_kernel_map_matches_the_committed_summary():
     """Every kernel that bench.load_pmc_traffic sums for a timed phase exists in the
     committed PMC summary of the default build (profiles/pmc_latest.json), so each
     priced phase of the bench line carries its measured traffic; the accumulate
-    phase is the sum of its two side-by-side kernels."""
+    phase is the sum of its two side-by-side kernels and k_hot_finish (same timer)."""
     sys.path.insert(0, REPO)
     import bench
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
@@ -149,7 +149,7 @@ def test_pmc_kernel_map_matches_the_committed_summary():
     for phase, kernels in bench.PMC_KERNELS.items():
         for k in kernels:
             assert k in ks and "hbm_bytes_per_launch" in ks[k], f"{phase}: {k} not in {path}"
-    assert set(bench.PMC_KERNELS["accum"]) == {"accum_cold_h", "accum_split"}
+    assert set(bench.PMC_KERNELS["accum"]) == {"accum_cold_h", "accum_split", "hot_finish"}
     pl = {"workload": pm["workload"], "count": pm["series"], "samples": pm["samples"]}
     from linkerd_amd import _native
     real = _native.engine_source_hash

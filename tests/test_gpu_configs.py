@@ -24,6 +24,8 @@ import pytest
 from linkerd_amd import _native as N
 from linkerd_amd import synth
 
+from .test_gpu_fullsize import _all_summaries_match_oracle
+
 pytestmark = pytest.mark.gpu
 THREADS = 16  # the GPU box's CPU share per GPU
 
@@ -280,6 +282,10 @@ def test_c4_product_sparse_merge_8_way_1m_series(oracle):
                 assert torch.equal(summ[r][:c], one_summ[f:f + c]), f"seed {seed} rank {r}: summaries vs one engine"
                 assert torch.equal(summ[r][:c, 0], truth[f:f + c].sum(dim=1, dtype=torch.int64))
                 assert torch.equal(summ[r][:c, 3], sums[f:f + c])
+                # every field of every series of the slice against the oracle's summary of
+                # the truth rows (Metric.scala:53-67), bytewise
+                _all_summaries_match_oracle(oracle, truth[f:f + c], sums[f:f + c], summ[r][:c],
+                                            f"seed {seed} rank {r}", first=f)
             del truth, sums, one_summ
             # bit-exact oracle replay of sampled series (head, direct/split, cold; every rank's slice)
             rng = np.random.default_rng(100 + seed)

@@ -88,6 +88,26 @@ def test_c3_full_size_invariants_and_sampled_oracle(oracle):
     torch.cuda.empty_cache()
 
 
+THREADS = 16  # the GPU box's CPU share per GPU
+
+
+def _all_summaries_match_oracle(oracle, truth, sums, summ, what, first=0):
+    """All 11 HistogramSummary fields of every row of `summ` (device [n][11] int64, avg as
+    its bits) == the oracle's summaries of the torch truth rows `truth` (device [n][1798])
+    with the exact totals `sums`, compared as bytes; a mismatch names its first series and
+    field (`first` offsets the series ids)."""
+    want = oracle.summarize_counts(truth.cpu().numpy(), sums.cpu().numpy(), threads=THREADS)
+    got = summ.cpu().numpy()
+    assert got.shape[0] == want.shape[0]
+    wb = want.view(np.int64).reshape(-1, 11)
+    if not np.array_equal(got, wb):
+        bad = np.nonzero((got != wb).any(axis=1))[0]
+        i = int(bad[0])
+        fld = [f for k, f in enumerate(N.SUMMARY_FIELDS) if got[i, k] != wb[i, k]]
+        raise AssertionError(f"{what}: {bad.size} summaries differ from the oracle; first series "
+                             f"{first + i} fields {fld}: {got[i].tolist()} vs {wb[i].tolist()}")
+
+
 def _gen_c3(lib, series, values, S, seed, stream):
     import torch
     cdf = torch.from_numpy(synth.zipf_cdf(S)).to(series.device)
@@ -142,6 +162,9 @@ def test_c3_whole_batches_bucket_exact(oracle):
             assert int(bad.sum()) == 0, f"seed {seed}: {int(bad.sum())} series differ, first {torch.nonzero(bad)[:8].flatten().tolist()}"
             assert torch.equal(summ[:, 0], truth.sum(dim=1, dtype=torch.int64)), f"seed {seed}: counts"
             assert torch.equal(summ[:, 3], sums), f"seed {seed}: sums"
+            # every field of every series' summary against the oracle's summary of the truth
+            # rows (Metric.scala:53-67, l5do_summary_of_counts per row), bytewise
+            _all_summaries_match_oracle(oracle, truth, sums, summ, f"seed {seed}")
             del truth, sums, bad
     finally:
         eng.close()

@@ -202,3 +202,7 @@ def test_summarize_counts_matches_hist():
     g = np.load(os.path.join(GOLDEN, "golden_mixed64.npz"))
     s = O.summarize_counts(g["counts"], g["totals"])
     assert s.view(np.uint8).reshape(-1, 88).tobytes() == g["summaries"].tobytes()
+    # the threaded batch driver (the full-size GPU tests' checker): same bytes at any split
+    for threads in (3, 8, 200):
+        t = O.summarize_counts(g["counts"], g["totals"], threads=threads)
+        assert t.tobytes() == s.tobytes()
