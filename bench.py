@@ -96,6 +96,9 @@ def parse():
     p.add_argument("--direct-max", type=int, default=None, help="engine param: direct tiles (0..255)")
     p.add_argument("--direct-div", type=int, default=None, help="engine param: direct-tile run divisor")
     p.add_argument("--variant", type=int, default=0, help="engine param L5DH_PARAM_VARIANT (A/B timing; 0: default)")
+    p.add_argument("--first-interval", action="store_true",
+                   help="plan every batch's partition regions as a first interval does (from its sample alone: "
+                        "variant bit 2)")
     p.add_argument("--hot-chunk", type=int, default=None, help="engine param L5DH_PARAM_HOT_CHUNK (records per big-tile item)")
     p.add_argument("--cpu-sample", type=int, default=None, help="samples in the CPU baseline sample (0: skip)")
     p.add_argument("--cpu-threads", type=int, default=None, help="oracle threads (default: c1 1, else the host's)")
@@ -400,7 +403,11 @@ def run_c4_loopback(args, result_out, check=True):
                                        "EXCLUDES the interconnect; modelled_xgmi_ms is a model of that term, not "
                                        "a measurement",
                    "modelled_xgmi_ms": round(xgmi_ms, 4),
-                   "modelled_xgmi": f"largest per-rank sent bytes / (W-1) links / {XGMI_LINK_GBS} GB/s per link"},
+                   "modelled_xgmi": f"largest per-rank sent bytes / (W-1) links / {XGMI_LINK_GBS} GB/s per link "
+                                    "(ideal links, no receive-side contention)",
+                   # the explicit sum: measured one-GPU rank time + the modelled interconnect term
+                   # (a model: not a fleet measurement)
+                   "per_rank_ms_loopback_plus_modelled_xgmi": round(ms / W + xgmi_ms, 4)},
         "path_roofline": {"bound": "hbm", "achieved": round(path_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(path_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_step": balg,
                           "formula": "8 B/sample + 7280 B/series for the fleet, once (SURVEY.md §8d)"},
@@ -486,7 +493,8 @@ def run(args):
 
     eng = HistogramEngine(S, device=torch.cuda.current_device())
     for prm, v in ((N_.PARAM_DIRECT_MAX, args.direct_max), (N_.PARAM_DIRECT_DIV, args.direct_div),
-                   (N_.PARAM_REGION_PCT, args.region_pct), (N_.PARAM_VARIANT, args.variant or None),
+                   (N_.PARAM_REGION_PCT, args.region_pct),
+                   (N_.PARAM_VARIANT, (args.variant | (4 if args.first_interval else 0)) or None),
                    (N_.PARAM_HOT_CHUNK, args.hot_chunk)):
         if v is not None:
             eng.set_param(prm, v)
@@ -551,6 +559,7 @@ def run(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    redo0 = eng.partition_redos()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -560,6 +569,7 @@ def run(args):
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    redo1 = eng.partition_redos()
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -658,6 +668,7 @@ def run(args):
         cfg = {"workload": wl_names[pl["workload"]], "series_total": pl["S_total"], "samples_per_step": total_samples,
                "series_per_gpu": S, "samples_per_gpu_per_step": n, "rotating_batches": R,
                **({"hot_shift": True} if args.hot_shift else {}),
+               **({"first_interval": True} if args.first_interval else {}),
                "parallelism": (f"sample-sharded x{world}" if fleet else
                                f"series-sharded x{world} (weighted ranges)" if pl["workload"] == "c3" else
                                f"replicas x{world}"),
@@ -679,6 +690,8 @@ def run(args):
                               "unit": "GB/s", "frac": round(path_gbs / (HBM_PEAK_GBS * gpus), 4),
                               "alg_bytes_per_step": balg, "formula": "8 B/sample + 7280 B/series (SURVEY.md §8d)"},
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+            # partition passes redone in the timed steps (a capacity-planned region overflowed)
+            "redos": {"level1": redo1[0] - redo0[0], "level2": redo1[1] - redo0[1], "steps": args.steps},
         }
         if merge:
             line["merge"] = merge

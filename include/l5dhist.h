@@ -77,7 +77,9 @@ enum {
                                   below 100 exercise that path (tests) and cost time, never results */
   L5DH_PARAM_VARIANT = 12      /* kernel variant bits for same-context A/B timing (0: the default kernels;
                                   every variant computes the same results; bit 0: one-tile folds in u16 bins;
-                                  bit 1: DMA copies of pinned host batches; other bits are ignored) */
+                                  bit 1: DMA copies of pinned host batches; bit 2: every ingest batch's
+                                  capacity plan made as for a first interval, from its sample alone;
+                                  other bits are ignored) */
 };
 
 /* Fleet-merge modes for l5dh_merge */
@@ -218,6 +220,11 @@ int l5dh_merge_all(l5dh_ctx** ctxs, int n, int mode, l5dh_summary** outs, int32_
  * / 32) entries; staged samples are binned first).  The load a series-sharded fleet
  * plans its next ranges from (linkerd_amd/fleet.py plan_shards). */
 int l5dh_tile_totals(l5dh_ctx* ctx, uint64_t* out, size_t n);
+
+/* Partition passes redone since l5dh_open because a capacity-planned region overflowed
+ * (any pointer nullable): *level1 / *level2 = redos of the level-1 / level-2 partition
+ * (each costs about one more pass of that level; results are exact either way). */
+int l5dh_partition_redos(l5dh_ctx* ctx, uint64_t* level1, uint64_t* level2);
 
 /* Bytes of the last l5dh_merge / l5dh_merge_all on this context (any pointer nullable):
  * *dense = the dense rows + totals a reduce-scatter would move ([S][1798] int32 +

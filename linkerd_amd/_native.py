@@ -93,6 +93,7 @@ SIGNATURES = {
     "l5dh_merge": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
     "l5dh_tile_totals": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.c_size_t]),
     "l5dh_merge_bytes": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
+    "l5dh_partition_redos": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
     "l5dh_merge_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.POINTER(_vp), _c.POINTER(_vp),
                                   _c.POINTER(_vp), _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
 }
@@ -136,6 +137,8 @@ def load(path: str = LIB_PATH):
                 "(or make -C linkerd_amd/csrc); there is no CPU fallback")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("L5DH_LIB") and not hasattr(lib, name):
+                continue  # (an A/B build of an older revision: entry points it predates are absent)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

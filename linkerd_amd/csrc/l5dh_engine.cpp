@@ -149,6 +149,42 @@ int build_bucket_lut2(const int32_t* L, uint32_t* lut2) {
   }
   return 0;
 }
+
+// Level 1's LUT (same intervals and index as lut2): entry {b0 | lim1 << 11, lim2}, the
+// absolute limits inside the interval (lim1 = 0x1FFFFF, lim2 = 0xFFFFFFFF: none), so
+// bucket = b0 + (v << 11 | 0x7FF >= x0) + (v >= x1) for v < V_ESC -- no interval start
+// or offset arithmetic on the device.  Verified exhaustively against upper_bound.
+int build_bucket_lut3(const int32_t* L, uint32_t* lut3) {
+  int k = 0;
+  auto entry = [&](int64_t start, int64_t end) {
+    const int b0 = host_bucket(L, start);
+    uint32_t lim[2] = {0x1FFFFFu, 0xFFFFFFFFu};
+    for (int i = 0; i < 2 && b0 + i < NL && L[b0 + i] <= end; ++i) {
+      if (L[b0 + i] <= start || L[b0 + i] >= 0x1FFFFF) return false;
+      lim[i] = (uint32_t)L[b0 + i];
+    }
+    if (b0 + 2 < NL && L[b0 + 2] <= end) return false;  // at most two limits per interval
+    if (b0 > 0x7FF) return false;
+    lut3[2 * k] = (uint32_t)b0 | lim[0] << 11;
+    lut3[2 * k + 1] = lim[1];
+    ++k;
+    return true;
+  };
+  for (int v = 0; v < 64; ++v)
+    if (!entry(v, v)) return 1;
+  for (int e = 6; e <= 20; ++e)
+    for (int m = 0; m < 64; ++m)
+      if (!entry((int64_t)(64 + m) << (e - 6), ((int64_t)(64 + m + 1) << (e - 6)) - 1)) return 1;
+  if (k != LUT2_N) return 1;
+  for (uint32_t v = 0; v < V_ESC; ++v) {  // the device index (lut3_index) and decode
+    const uint32_t sh = (uint32_t)(25 - __builtin_clz(v | 64u));
+    const uint32_t idx = (v >> sh) + (sh << 6);
+    const uint32_t x0 = lut3[2 * idx], x1 = lut3[2 * idx + 1];
+    const uint32_t b = (x0 & 0x7FFu) + ((v << 11 | 0x7FFu) >= x0 ? 1u : 0u) + (v >= x1 ? 1u : 0u);
+    if ((int)b != host_bucket(L, v)) return 2;
+  }
+  return 0;
+}
 }  // namespace l5dh
 
 struct l5dh_ctx {
@@ -354,7 +390,7 @@ int ensure(l5dh_ctx* c, DevBuf& b, size_t bytes) {
   return 0;
 }
 
-Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2}; }
+Tables tables(l5dh_ctx* c) { return Tables{c->d_lim_pad, c->d_mid, c->d_base, c->d_lut, c->d_lut2, c->d_lut2 + LUT2_N}; }
 
 State state(l5dh_ctx* c) { return State{c->d_counts, c->d_total, c->d_sumfix, c->d_dirty, c->S, c->F}; }
 
@@ -551,6 +587,9 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   a.vec = vec;
   {
     KTimer kt(c, L5DH_K_SCAN);
+    // variant bit 2 (measurement): forget the previous batch's exact key counts, so every
+    // batch is planned as a first interval is -- from its sample alone
+    if (c->variant & 4) HIPCHK(c, hipMemsetAsync(c->d_kprev, 0, (size_t)2 * c->F * 4, c->stream));
     HIPCHK(c, launch_ingest(a, 0, c->stream));
   }
   {
@@ -1119,7 +1158,7 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   const size_t S = c->S, F = c->F;
   auto mal = [&](void** p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 256)) == hipSuccess; };
   bool ok = mal((void**)&c->d_lim_pad, LIM_PAD * 4) && mal((void**)&c->d_mid, NB * 4) &&
-            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 8) && mal((void**)&c->d_counts, S * ROW * 4) &&
+            mal((void**)&c->d_base, ROW * 4) && mal((void**)&c->d_lut, LUT_N * 4) && mal((void**)&c->d_lut2, LUT2_N * 16) && mal((void**)&c->d_counts, S * ROW * 4) &&
             mal((void**)&c->d_total, S * 8) && mal((void**)&c->d_sumfix, S * 8) && mal((void**)&c->d_dirty, F) &&
             mal((void**)&c->d_err, 4) && mal((void**)&c->d_tile_tot, F * 4) &&
             mal((void**)&c->d_cold_item, (F + 1) * 16) && mal((void**)&c->d_hot_list, F * 4) &&
@@ -1128,7 +1167,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
             mal((void**)&c->d_enc_dw, 2 * F * 4) &&
             mal((void**)&c->d_kest, 2 * F * 4) && mal((void**)&c->d_kprev, 2 * F * 4);
   const size_t meta_bytes = (size_t)meta_layout((uint32_t)F).words() * 4;
-  for (int j = 0; ok && j < MAX_SEG; ++j) ok = mal((void**)&c->segs[j].meta, meta_bytes);
+  for (int j = 0; ok && j < MAX_SEG; ++j)  // (zeroed: the header's redo counters only grow)
+    ok = mal((void**)&c->segs[j].meta, meta_bytes) && hipMemset(c->segs[j].meta, 0, meta_bytes) == hipSuccess;
   if (!ok) {
     (void)hipGetLastError();
     return bail(-ENOMEM);
@@ -1145,8 +1185,8 @@ int l5dh_open(l5dh_ctx** out, uint32_t max_series, uint32_t device_mask) {
   }
   uint32_t lut[LUT_N];
   if (build_bucket_lut(hl.L, lut) > 2) return bail(-EIO);
-  static uint32_t lut2[2 * LUT2_N];
-  static int lut2_rc = build_bucket_lut2(hl.L, lut2);  // built and verified once per process
+  static uint32_t lut2[4 * LUT2_N];  // lut2, then lut3 (d_lut2 holds both)
+  static int lut2_rc = build_bucket_lut2(hl.L, lut2) | build_bucket_lut3(hl.L, lut2 + 2 * LUT2_N);  // once per process
   if (lut2_rc != 0) return bail(-EIO);
   if (hipMemcpy(c->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->d_lut2, lut2, sizeof(lut2), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1618,6 +1658,28 @@ int l5dh_tile_totals(l5dh_ctx* c, uint64_t* out, size_t n) {
   HIPCHK(c, hipMemcpyAsync(k.data(), c->d_kprev, k.size() * 4, hipMemcpyDeviceToHost, c->stream));
   if ((r = sync_stream(c))) return r;
   for (uint32_t t = 0; t < c->F; ++t) out[t] = (uint64_t)k[2 * t] + k[2 * t + 1];
+  return 0;
+}
+
+int l5dh_partition_redos(l5dh_ctx* c, uint64_t* level1, uint64_t* level2) {
+  if (!c) return -EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int r;
+  if ((r = flush_ring(c))) return r;
+  const MetaLayout L = meta_layout(c->F);
+  uint32_t h[MAX_SEG][2] = {};
+  if (c->F > 1)
+    for (int j = 0; j < MAX_SEG; ++j)
+      HIPCHK(c, hipMemcpyAsync(h[j], c->segs[j].meta + L.hdr() + H_NOVR1, 8, hipMemcpyDeviceToHost, c->stream));
+  if ((r = sync_stream(c))) return r;
+  uint64_t a = 0, b = 0;
+  for (int j = 0; j < MAX_SEG; ++j) {
+    a += h[j][0];
+    b += h[j][1];
+  }
+  if (level1) *level1 = a;
+  if (level2) *level2 = b;
   return 0;
 }
 

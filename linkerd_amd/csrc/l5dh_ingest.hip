@@ -27,6 +27,7 @@
 // Final record (rec16, direct tiles at level 1, the others at level 2): [15:11]
 //   series in tile | [10:0] bucket.
 #include <algorithm>
+#include <type_traits>
 
 #include "l5dh_device.hpp"
 
@@ -628,6 +629,15 @@ __global__ __launch_bounds__(NT) void k_rbin1w(const uint32_t* __restrict__ seri
   }
 }
 
+// lut3: byte offset of key v's entry (v < 2^21; the lut2 intervals), and its bucket
+__device__ __forceinline__ uint32_t lut3_byte(uint32_t v) {
+  const uint32_t sh = 25u - (uint32_t)__builtin_clz(v | 64u);
+  return ((v >> sh) + (sh << 6)) << 3;
+}
+__device__ __forceinline__ uint32_t lut3_bucket(uint32_t v, uint2 x) {
+  return (x.x & 0x7FFu) + (((v << 11) | 0x7FFu) >= x.x ? 1u : 0u) + (v >= x.y ? 1u : 0u);
+}
+
 // ------------------------------------------------------------------------
 // After level 1 (one workgroup, thread = bin): exact bin totals, the direct keys'
 // ranges, and on an overflow exact regions for the redo pass (super-tile bins in
@@ -790,10 +800,10 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   // level-1 records: words of `meta` this kernel only reads (wave-uniform: scalar loads)
   constexpr int PT = (int)ITEM2 / NT;
   constexpr int PG = PT / 4;  // 16-B groups per thread
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ __attribute__((aligned(16))) uint32_t smem[rbin2_lds() / 4];  // (static: constant LDS addresses)
   unsigned long long* lsum = reinterpret_cast<unsigned long long*>(smem);  // [2048]
-  uint2* lut2 = reinterpret_cast<uint2*>(lsum + 2048);                     // [LUT2_N]
-  uint2* ocx = lut2 + LUT2_N;                                              // [2][B2_KEYS] {stage offset, run base}
+  uint2* lut3 = reinterpret_cast<uint2*>(lsum + 2048);                     // [LUT2_N]
+  uint2* ocx = lut3 + LUT2_N;                                              // [2][B2_KEYS] {stage offset, run base}
   uint32_t* cnt = reinterpret_cast<uint32_t*>(ocx + 2 * B2_KEYS);          // [B2_KEYS + 64]: a spare per lane
   uint32_t* stage = cnt + B2_KEYS + 64;                                    // [2][ITEM2] {rec16 | key << 16}, sorted
   const MetaLayout L = meta_layout(F);
@@ -808,7 +818,7 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
   const uint32_t* kbase = meta + L.kbase();
   const uint32_t* kcap = meta + L.kcap();
   const int lane = lane_id(), wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < LUT2_N; i += NT) lut2[i] = tb.lut2[i];
+  for (int i = threadIdx.x; i < LUT2_N; i += NT) lut3[i] = tb.lut3[i];
   for (int i = threadIdx.x; i < 2048; i += NT) lsum[i] = 0ull;
   for (int i = threadIdx.x; i < B2_KEYS; i += NT) cnt[i] = 0u;
   // super-tile of the first item: the last j with istart[j] <= i0 (empty super-tiles
@@ -909,31 +919,47 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       for (int g = 0; g < PG; ++g) {
         r[4 * g] = x[g].x; r[4 * g + 1] = x[g].y; r[4 * g + 2] = x[g].z; r[4 * g + 3] = x[g].w;
       }
-      // The rank and value-sum atomics carry no control flow: an invalid slot (past the
-      // item's end) counts into a spare word of its lane and every slot adds to a sum (0
-      // when it has nothing to add), so the atomics of consecutive slots stay in flight
-      // together.  The branchy form (rank = valid ? atomicAdd : 0, sum under an if) had an
-      // lgkmcnt(0) wait behind every rank atomic (round 5).
-      // LUT reads batched per half (all 12 at once, or the scatter / write-out batches of 12
-      // instead of 4: level 2 +0.01..+0.03 ms, round 5)
-      constexpr int H = PT / 2;
+      // A whole item with no escaped record in the wave (nearly every item) takes the lean
+      // form: key = r >> 25 (tile in super-tile, half), lsum index = r >> 21 (tile, series),
+      // the bucket from lut3, no validity or escape selects (round 5's form issued ~45 VALU
+      // instructions per record).  The careful form (the item's ragged end, escapes, the
+      // redo pass): the rank and value-sum atomics carry no control flow -- an invalid slot
+      // counts into a spare word of its lane and every slot adds to a sum (0 when it has
+      // nothing to add) -- so the atomics of consecutive slots stay in flight together.
+      bool escq = false;
 #pragma unroll
-      for (int k = 0; k < PT; ++k) {
-        uint2 lv[H];
-        if (k % H == 0) {
+      for (int k = 0; k < PT; ++k) escq |= (r[k] & 0x1FFFFFu) >= V_ESC;
+      const bool lean = ctot == ITEM2 && pass == 0 && !__ballot(escq);
+      constexpr int H = PT / 2;  // LUT reads batched per half
+      if (lean) {
 #pragma unroll
-          for (int q = 0; q < H; ++q) lv[q] = lut2[lut2_index(r[k + q] & 0x1FFFFFu)];
+        for (int k = 0; k < PT; ++k) {
+          uint2 lv[H];
+          if (k % H == 0) {
+#pragma unroll
+            for (int q = 0; q < H; ++q) lv[q] = lut3[lut3_byte(r[k + q] & 0x1FFFFFu) >> 3];
+          }
+          const uint32_t p = r[k] & 0x1FFFFFu;
+          kr[k] = ((r[k] >> 25) << 16) | ((r[k] >> 10) & 0xF800u) | lut3_bucket(p, lv[k % H]);
+          rank[k] = atomicAdd(&cnt[r[k] >> 25], 1u);
+          atomicAdd(&lsum[(r[k] >> 21) & 2047u], (unsigned long long)p);
         }
-        const uint32_t p = r[k] & 0x1FFFFFu;
-        uint32_t o;
-        const uint32_t bk = lut2_decode(p, lv[k % H], o);
-        const bool esc = p >= V_ESC;
-        const uint32_t bucket = sel_u32(esc, p - V_ESC, bk);
-        const uint32_t sl = (r[k] >> 21) & 31u, tl = r[k] >> 26;
-        const bool valid = 4u * ((uint32_t)(k >> 2) * NT + threadIdx.x) + (uint32_t)(k & 3) < ctot;
-        kr[k] = valid ? ((sl << 11) | bucket | ((2u * tl + (sl >> 4)) << 16)) : NOKEY;
-        rank[k] = atomicAdd(&cnt[valid ? kr[k] >> 16 : (uint32_t)B2_KEYS + (uint32_t)lane], 1u);
-        atomicAdd(&lsum[tl * 32u + sl], (unsigned long long)((pass == 0 && valid && !esc && p) ? p : 0u));
+      } else {
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+          uint2 lv[H];
+          if (k % H == 0) {
+#pragma unroll
+            for (int q = 0; q < H; ++q) lv[q] = lut3[lut3_byte(r[k + q] & 0x1FFFFFu) >> 3];
+          }
+          const uint32_t p = r[k] & 0x1FFFFFu;
+          const bool esc = p >= V_ESC;
+          const uint32_t bucket = sel_u32(esc, p - V_ESC, lut3_bucket(p, lv[k % H]));
+          const bool valid = 4u * ((uint32_t)(k >> 2) * NT + threadIdx.x) + (uint32_t)(k & 3) < ctot;
+          kr[k] = valid ? (((r[k] >> 25) << 16) | ((r[k] >> 10) & 0xF800u) | bucket) : NOKEY;
+          rank[k] = atomicAdd(&cnt[valid ? r[k] >> 25 : (uint32_t)B2_KEYS + (uint32_t)lane], 1u);
+          atomicAdd(&lsum[(r[k] >> 21) & 2047u], (unsigned long long)((pass == 0 && valid && !esc) ? p : 0u));
+        }
       }
     }
     __syncthreads();  // B1: counts complete
@@ -970,9 +996,11 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
         uint32_t o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = oc[(kr[k0 + j] >> 16) & (B2_KEYS - 1)].x;
+        // (an invalid slot's record goes to its lane's spare counter word -- written by
+        // nothing else in this phase, read by nothing -- instead of a branch per slot)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (kr[k0 + j] != NOKEY) st[o[j] + rank[k0 + j]] = kr[k0 + j];
+          *(kr[k0 + j] != NOKEY ? &st[o[j] + rank[k0 + j]] : &cnt[B2_KEYS + lane]) = kr[k0 + j];
       }
     }
     PH2_MARK(2)
@@ -1093,10 +1121,8 @@ hipError_t set_ingest_attributes() {
     return e;
   if ((e = hipFuncSetAttribute((const void*)k_rplan1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RPLAN1_LDS)))
     return e;
-  if ((e = hipFuncSetAttribute((const void*)k_rbin1w<NT1, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)rbin1w_lds())))
-    return e;
-  return hipFuncSetAttribute((const void*)k_rbin2<B2_NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbin2_lds());
+  return hipFuncSetAttribute((const void*)k_rbin1w<NT1, CHW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)rbin1w_lds());
 }
 
 hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
@@ -1126,7 +1152,7 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
       const uint32_t B = (K + 1023) / 1024;
       for (int pass = 0; pass < 2; ++pass) {
         const MetaLayout L = meta_layout(a.F);
-        hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(a.num_cu * B2_PER_CU), dim3(B2_NT), rbin2_lds(), st, a.S, a.F, a.tb, a.meta,
+        hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(a.num_cu * B2_PER_CU), dim3(B2_NT), 0, st, a.S, a.F, a.tb, a.meta,
                            a.meta + L.istart(), a.meta + L.bbase(), a.meta + L.btot(), a.rec32, a.rec16, a.sumfix,
                            pass);
         if (pass == 0) {

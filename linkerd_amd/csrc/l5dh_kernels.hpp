@@ -52,6 +52,7 @@ struct Tables {            // constant tables in HBM (a few KB each, L2 resident
   const int32_t* base;     // [1800] lower limit of bucket b (0 for b == 0), zero padded
   const uint32_t* lut;     // [LUT_N] bucket bracket + in-interval limit offsets (bucket_lut)
   const uint2* lut2;       // [LUT2_N] {o1 | o2 << 16, b0 | p << 16} (bucket_lut2)
+  const uint2* lut3;       // [LUT2_N] {b0 | lim1 << 11, lim2}: level 1's decode (build_bucket_lut3)
 };
 
 // ---- binned segments (one ingest batch each) -------------------------------
@@ -230,5 +231,6 @@ hipError_t set_snapshot_attributes();
 int build_bucket_lut(const int32_t* limits, uint32_t* lut);
 // LUT for bucket_lut2 (keys < 2^21), verified exhaustively; 0 on success.
 int build_bucket_lut2(const int32_t* limits, uint32_t* lut2);
+int build_bucket_lut3(const int32_t* limits, uint32_t* lut3);
 
 }  // namespace l5dh
