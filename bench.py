@@ -691,7 +691,10 @@ def run(args):
                               "alg_bytes_per_step": balg, "formula": "8 B/sample + 7280 B/series (SURVEY.md §8d)"},
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
             # partition passes redone in the timed steps (a capacity-planned region overflowed)
-            "redos": {"level1": redo1[0] - redo0[0], "level2": redo1[1] - redo0[1], "steps": args.steps},
+            # (level2_counted: batches whose level-2 regions were known not to fit after
+            # level 1 -- the first level-2 pass only counted, the second wrote exact regions)
+            "redos": {"level1": redo1[0] - redo0[0], "level2": redo1[1] - redo0[1],
+                      "level2_counted": redo1[2] - redo0[2], "steps": args.steps},
         }
         if merge:
             line["merge"] = merge

@@ -223,8 +223,11 @@ int l5dh_tile_totals(l5dh_ctx* ctx, uint64_t* out, size_t n);
 
 /* Partition passes redone since l5dh_open because a capacity-planned region overflowed
  * (any pointer nullable): *level1 / *level2 = redos of the level-1 / level-2 partition
- * (each costs about one more pass of that level; results are exact either way). */
-int l5dh_partition_redos(l5dh_ctx* ctx, uint64_t* level1, uint64_t* level2);
+ * (each costs about one more pass of that level; results are exact either way).
+ * *level2_counted = batches whose level-2 regions were known not to fit after level 1
+ * (a moved load, a first interval): their first level-2 pass only counted the keys
+ * (about 0.4 of a pass) and the second wrote exact regions -- not counted as redos. */
+int l5dh_partition_redos(l5dh_ctx* ctx, uint64_t* level1, uint64_t* level2, uint64_t* level2_counted);
 
 /* Bytes of the last l5dh_merge / l5dh_merge_all on this context (any pointer nullable):
  * *dense = the dense rows + totals a reduce-scatter would move ([S][1798] int32 +

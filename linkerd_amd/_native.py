@@ -93,7 +93,8 @@ SIGNATURES = {
     "l5dh_merge": (_c.c_int, [_vp, _c.c_int, _vp, _vp, _vp, _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
     "l5dh_tile_totals": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.c_size_t]),
     "l5dh_merge_bytes": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
-    "l5dh_partition_redos": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64)]),
+    "l5dh_partition_redos": (_c.c_int, [_vp, _c.POINTER(_c.c_uint64), _c.POINTER(_c.c_uint64),
+                                        _c.POINTER(_c.c_uint64)]),
     "l5dh_merge_all": (_c.c_int, [_c.POINTER(_vp), _c.c_int, _c.c_int, _c.POINTER(_vp), _c.POINTER(_vp),
                                   _c.POINTER(_vp), _c.POINTER(_c.c_uint32), _c.POINTER(_c.c_uint32)]),
 }

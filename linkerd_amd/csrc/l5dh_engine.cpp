@@ -1661,25 +1661,28 @@ int l5dh_tile_totals(l5dh_ctx* c, uint64_t* out, size_t n) {
   return 0;
 }
 
-int l5dh_partition_redos(l5dh_ctx* c, uint64_t* level1, uint64_t* level2) {
+int l5dh_partition_redos(l5dh_ctx* c, uint64_t* level1, uint64_t* level2, uint64_t* level2_counted) {
   if (!c) return -EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
   int r;
   if ((r = flush_ring(c))) return r;
   const MetaLayout L = meta_layout(c->F);
-  uint32_t h[MAX_SEG][2] = {};
+  static_assert(H_NOVR2 == H_NOVR1 + 1 && H_NCNT2 == H_NOVR1 + 3, "header words read together");
+  uint32_t h[MAX_SEG][4] = {};
   if (c->F > 1)
     for (int j = 0; j < MAX_SEG; ++j)
-      HIPCHK(c, hipMemcpyAsync(h[j], c->segs[j].meta + L.hdr() + H_NOVR1, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(h[j], c->segs[j].meta + L.hdr() + H_NOVR1, 16, hipMemcpyDeviceToHost, c->stream));
   if ((r = sync_stream(c))) return r;
-  uint64_t a = 0, b = 0;
+  uint64_t a = 0, b = 0, k = 0;
   for (int j = 0; j < MAX_SEG; ++j) {
     a += h[j][0];
     b += h[j][1];
+    k += h[j][3];
   }
   if (level1) *level1 = a;
   if (level2) *level2 = b;
+  if (level2_counted) *level2_counted = k;
   return 0;
 }
 

@@ -45,26 +45,41 @@ constexpr size_t RPLAN1_LDS = 32 * 1024 * 4;  // k_rplan1's per-tile sampled ids
 __device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
 // Region capacity of a bin or key from the previous batch's exact records `prev`
-// and this batch's sampled ids `e` (scale s = samples per draw): when the sample is
-// consistent with the previous batch (e within 4 sigma above prev / s) the previous
-// count +1/16 + 4 sigma; when it is not (a key that grew, or one never seen) the
-// sample's estimate + 4 sigma; exact when the sample was the whole batch.  Plus a
-// pad.  A region that still overflows is redone with exact sizes (k_rfix1 /
-// k_rfix2), so this only has to be right almost always -- but taking the larger of
-// both bounds always would oversize every key by the sample's 4 sigma (C2: 1.3x, past
-// the region buffer).  `pct` scales the result (L5DH_PARAM_REGION_PCT; below 100
-// forces the redo path).
+// and this batch's sampled ids `e` (scale s = samples per draw).  The sample's bound
+// is a Poisson upper bound on the mean, (sqrt(e + 1) + z / 2)^2 draws: e + z sigma
+// alone is short for the few draws of a tail bin (C3: 20-80).  When the sample is
+// consistent with the previous batch (e within 4 sigma above and 6 sigma below
+// prev / s) the previous count +1/16 + 4 sigma, and for a level-1 super-tile bin
+// (`floor_sample`) at least the sample's bound; otherwise (a key that grew or shrank,
+// or one never seen) the sample's bound; exact when the sample was the whole batch.
+// Plus a pad.  A region that still overflows is redone with exact sizes (k_rfix1 /
+// k_rfix2), so this only has to be right almost always -- but the sample's bound for
+// every level-2 key would oversize each by ~z sigma (C2: 1.3x, past the region buffer).
+// Round 6 (C3 --hot-shift, a moved hot set: every level-1 pass was redone,
+// profiles/r06fin1_c3hot_bench.json; simulated in tools/plan_sim.py): a super-tile bin
+// whose load doubled, sampled at ~80 draws, still fell within 4 sigma of its previous
+// count -- hence the sample floor for those bins, whose buffer has room (C3 uses a
+// third of it); a bin that lost its hot series kept the old count's region and the
+// plan outgrew the buffer -- hence the lower test.  (6 sigma below: at 4, ~3000 well
+// sampled C3 keys would take a sample-sized region, about their true count, by chance
+// in ~10 % of steady-state batches.)  `pct` scales the result (L5DH_PARAM_REGION_PCT;
+// below 100 forces the redo path).
 __device__ __forceinline__ uint32_t rcap(double prev, double e, double s, bool exact, double pad, uint32_t align,
-                                         uint32_t pct) {
+                                         uint32_t pct, double z, bool floor_sample) {
   double c;
   if (exact) {
     c = e;
   } else {
-    const double e0 = prev / s;
-    if (prev > 0.0 && e <= e0 + 4.0 * sqrt(e0 + 1.0))
-      c = ceil(prev * 1.0625 + 4.0 * sqrt(prev)) + pad;
-    else
-      c = ceil((e + 4.0 * sqrt(e + 1.0)) * s) + pad;
+    const double e0 = prev / s, sg = sqrt(e0 + 1.0);
+    const double r = sqrt(e + 1.0) + 0.5 * z;
+    const double sb = ceil(r * r * s);
+    if (prev > 0.0 && e >= e0 - 6.0 * sg && (floor_sample || e <= e0 + 4.0 * sg)) {
+      c = ceil(prev * 1.0625 + 4.0 * sqrt(prev));
+      if (floor_sample) c = fmax(c, sb);
+    } else {
+      c = sb;
+    }
+    c += pad;
   }
   if (pct != 100) c = floor(c * (double)pct / 100.0);
   return round_up((uint32_t)fmin(c, 1073741824.0), align);
@@ -234,14 +249,15 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   E += __shfl_xor(E, 1, 64);
   if ((j & 1u) == 0 && (j >> 1) < FS) {
     const uint32_t b = j >> 1;
-    capl[b] = rcap(P, E, s, exact, 256.0, 4, pct);
+    capl[b] = rcap(P, E, s, exact, 256.0, 4, pct, 6.0, true);
+    meta[L.btot() + b] = (uint32_t)fmin(P, 4294967295.0);  // the bin's previous load, for k_rfix1
   }
   __syncthreads();  // dl complete
   const uint32_t TB = FS + 2 * ND;
   if (j >= FS && j < TB) {  // direct half-bins
     const uint32_t t = dl[(j - FS) >> 1], h = (j - FS) & 1u;
     const double p = (double)kprev[2 * t + h], e = (double)kest[2 * t + h];
-    capl[j] = rcap(p, e, s, exact, 256.0, 8, pct);  // (u16 records: 16-B aligned regions)
+    capl[j] = rcap(p, e, s, exact, 256.0, 8, pct, 5.0, false);  // (u16 records: 16-B aligned regions)
   }
   __syncthreads();
   // two address spaces: super-tile bins in rec32, the direct half-bins in rec16 below
@@ -264,6 +280,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_REDO1] = 0;
     hdr[H_OV2] = 0;
     hdr[H_REDO2] = 0;
+    hdr[H_COUNT2] = 0;
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
@@ -655,6 +672,15 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
   const uint32_t b = threadIdx.x;
   const bool stb = b < FS, dj = b >= FS && b < TB;
   const uint32_t c = b < TB ? meta[L.bcnt() + b] : 0u;
+  // A super-tile whose records outgrew the bound its keys' level-2 regions were sized
+  // by (their previous counts +1/16 + 4 sigma; k_rplan1 left that count in btot): its
+  // load moved, or this is a first interval.  Its keys' regions (sampled at ~1 draw
+  // per key) would overflow, so level 2's first pass only counts, and the second
+  // writes into exact regions -- not a whole pass written, dropped and redone.
+  if (stb && !hdr[H_EXACT]) {
+    const double P = (double)meta[L.btot() + b];
+    if ((double)c > P * 1.0625 + 4.0 * sqrt(P) + 256.0) hdr[H_COUNT2] = 1u;
+  }
   meta[L.btot() + b] = c;
   uint32_t t32, t16;
   const uint32_t nb32 = block_excl_scan<1024>(stb ? round_up(c, 4) : 0u, lds, &t32);
@@ -689,7 +715,10 @@ __global__ __launch_bounds__(1024) void k_rfix1(uint32_t F, uint32_t* __restrict
   if (b == 0) {
     meta[L.istart() + FS] = all;
     hdr[H_ITEMS] = all;
-    if (ov && t16 > d16) hdr[H_D16] = t16;
+    if (ov && t16 > d16) {
+      hdr[H_D16] = t16;
+      hdr[H_COUNT2] = 1u;
+    }
     hdr[H_OV2] = 0u;
     hdr[H_REDO2] = 0u;
     hdr[H_REDO1] = ov;
@@ -736,7 +765,7 @@ __global__ __launch_bounds__(1024) void k_rplan2a(size_t n, uint32_t F, uint32_t
     const uint32_t e = kest[k];
     if (e) kest[k] = 0;  // ready for the next batch
     if (!tile_direct(meta, L, k >> 1)) {
-      cap = rcap((double)kprev[k], (double)e, s, exact, 32.0, 8, pct);
+      cap = rcap((double)kprev[k], (double)e, s, exact, 32.0, 8, pct, 5.0, false);
       meta[L.kcap() + k] = cap;
     }
   }
@@ -754,7 +783,7 @@ __global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restri
   __shared__ uint64_t red[16];
   __shared__ uint64_t l64[17];
   const MetaLayout L = meta_layout(F);
-  const uint32_t* hdr = meta + L.hdr();
+  uint32_t* hdr = meta + L.hdr();
   const uint64_t before = wsum_before(reinterpret_cast<const uint64_t*>(meta + L.wsum()), blockIdx.x, red);
   const uint32_t k = blockIdx.x * 1024u + threadIdx.x;
   const bool mine = k < L.K && !tile_direct(meta, L, k >> 1);
@@ -762,7 +791,10 @@ __global__ __launch_bounds__(1024) void k_rplan2b(uint32_t F, uint32_t* __restri
   uint64_t total;
   const uint64_t base = hdr[H_D16] + before + block_excl_scan64((uint64_t)cap, l64, &total);
   if (mine) {
-    if (base + cap + 64 > cap16) cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;  // clamped
+    if (base + cap + 64 > cap16) {  // clamped: level 2's first pass only counts (k_rbin2)
+      cap = base + 64 < cap16 ? (uint32_t)(cap16 - 64 - base) & ~7u : 0u;
+      hdr[H_COUNT2] = 1u;
+    }
     meta[L.kbase() + k] = (uint32_t)base;
     meta[L.kcap() + k] = cap;
     meta[L.kcnt() + k] = 0u;
@@ -856,6 +888,54 @@ __global__ __launch_bounds__(NT, B2_PER_CU * NT / 256) void k_rbin2(uint32_t S, 
       lsum[i] = 0ull;
     }
   };
+  // Count-only first pass (H_COUNT2: k_rplan2b clamped a region, or k_rfix1 saw a
+  // super-tile outgrow its keys' regions): the keys' exact counts and the value sums --
+  // no bucket, stage or write-out, non-returning atomics; k_rfix2 then lays the regions
+  // out exactly and the second pass writes them.
+  if (pass == 0 && __builtin_amdgcn_readfirstlane(hdr[H_COUNT2]) != 0u) {
+    uint32_t j, a, e;
+    item_range(i0, j, a, e);
+    uint4 x[PG];
+    load(a, e, x);
+    for (uint32_t item = i0; item < i1; ++item) {
+      const uint32_t cj = j, ctot = e - a;
+      uint4 xn[PG];
+      if (item + 1 < i1) item_range(item + 1, j, a, e);
+      load(a, e, xn);
+      if (cj != cur_j) {
+        if (cur_j != 0xFFFFFFFFu) {
+          __syncthreads();
+          flush(cur_j);
+        }
+        cur_j = cj;
+        __syncthreads();
+      }
+#pragma unroll
+      for (int g = 0; g < PG; ++g) {
+        const uint32_t rr[4] = {x[g].x, x[g].y, x[g].z, x[g].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t p = rr[q] & 0x1FFFFFu;
+          const bool valid = 4u * ((uint32_t)g * NT + threadIdx.x) + (uint32_t)q < ctot;
+          atomicAdd(&cnt[valid ? rr[q] >> 25 : (uint32_t)B2_KEYS + (uint32_t)lane], 1u);
+          atomicAdd(&lsum[(rr[q] >> 21) & 2047u], (unsigned long long)((valid && p < V_ESC) ? p : 0u));
+        }
+      }
+      __syncthreads();
+      if (wv < 2) {
+        const uint32_t rk = (uint32_t)wv * 64u + (uint32_t)lane;
+        const uint32_t rc = cnt[rk];
+        if (rc) atomicAdd(&kcnt[cj * (uint32_t)B2_KEYS + rk], rc);
+        cnt[rk] = 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < PG; ++g) x[g] = xn[g];
+    }
+    __syncthreads();
+    flush(cur_j);
+    return;
+  }
   // write-out of a sorted stage (each wave a contiguous range)
   // (in batches of 4 entries whose LDS reads go out together: entries past the end are
   // read too -- stale stage words, their key masked into range -- and not stored)
@@ -1056,7 +1136,7 @@ __global__ __launch_bounds__(1024) void k_rfix2a(uint32_t F, uint32_t* __restric
     uint64_t t = 0;
     for (int q = 0; q < 16; ++q) t += red[q];
     reinterpret_cast<uint64_t*>(meta + L.wsum())[blockIdx.x] = t;
-    if (blockIdx.x == 0) hdr[H_REDO2] = hdr[H_OV2];
+    if (blockIdx.x == 0) hdr[H_REDO2] = hdr[H_OV2] | hdr[H_COUNT2];
   }
 }
 
@@ -1078,8 +1158,9 @@ __global__ __launch_bounds__(1024) void k_rfix2b(uint32_t F, uint32_t* __restric
     meta[L.kcnt() + k] = 0u;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (hdr[H_COUNT2]) hdr[H_NCNT2] += 1u;  // a counting first pass, not a redo
+    else hdr[H_NOVR2] += 1u;
     hdr[H_OV2] = 0u;
-    hdr[H_NOVR2] += 1u;
   }
 }
 

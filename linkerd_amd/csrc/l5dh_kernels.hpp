@@ -89,11 +89,13 @@ enum : uint32_t {
   H_OV2 = 3,      // a level-2 run did not fit its region
   H_REDO2 = 4,    // level 2 runs again with exact regions
   H_ITEMS = 5,    // level-2 items
-  // (6-8: unused)
+  H_COUNT2 = 6,   // level 2's regions are known not to fit: its first pass only counts
+  // (7-8: unused)
   H_EXACT = 9,    // 1: every sample of the batch was counted by k_rsample
   H_NOVR1 = 10,   // level-1 redos (diagnostics, monotonic per segment slot)
-  H_NOVR2 = 11,
-  H_D16 = 12      // rec16 records reserved for the direct keys' regions (level-2 regions follow)
+  H_NOVR2 = 11,   // level-2 redos after an overflow
+  H_D16 = 12,     // rec16 records reserved for the direct keys' regions (level-2 regions follow)
+  H_NCNT2 = 13    // level-2 counting first passes (H_COUNT2; monotonic)
 };
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 

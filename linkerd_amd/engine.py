@@ -318,13 +318,14 @@ class HistogramEngine:
         return out
 
     def partition_redos(self):
-        """l5dh_partition_redos: (level-1, level-2) partition passes redone since open."""
-        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        """l5dh_partition_redos: (level-1 redos, level-2 redos, level-2 counting first
+        passes) since open."""
+        a, b, k = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         if not hasattr(self._lib, "l5dh_partition_redos"):  # (an older A/B build, L5DH_LIB)
-            return 0, 0
-        self._check(self._lib.l5dh_partition_redos(self._ctx, ctypes.byref(a), ctypes.byref(b)),
+            return 0, 0, 0
+        self._check(self._lib.l5dh_partition_redos(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(k)),
                     "l5dh_partition_redos")
-        return a.value, b.value
+        return a.value, b.value, k.value
 
     def merge_bytes(self) -> dict:
         """l5dh_merge_bytes: dense / encoded / sent bytes of the last merge."""

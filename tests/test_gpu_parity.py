@@ -531,3 +531,28 @@ def test_direct_run_delta_at_region_start(oracle, n):
         np.testing.assert_array_equal(totals, o.totals())
     finally:
         eng.close()
+
+
+def test_moving_load_counts_level2_first(oracle):
+    """A first interval and a hot set that moves (C3's Zipf head rotated by a third of
+    the series space between batches, as bench.py --hot-shift does): no level-1 redo
+    (rcap's two-sided consistency test sizes a bin that lost its load from the
+    sample, so the plan fits the buffer), and level 2 counts its keys first instead
+    of writing a pass that overflows and is redone (k_rfix1 sees the super-tiles
+    outgrow their previous loads); a steady batch of the same load does neither.
+    Counts and summaries exact throughout."""
+    S, n = 300_000, 3_000_000
+    eng = _engine(S)
+    o = oracle.OracleHistograms(S)
+    hist = []
+    for seed, shift in [(1, 0), (2, 0), (3, S // 3), (4, 2 * S // 3)]:
+        s, v = synth.c3(S=S, N=n, seed=seed)
+        s = ((s.astype(np.int64) + shift) % S).astype(np.uint32)
+        eng.ingest(s, v)
+        o.ingest(s, v, threads=8)
+        hist.append(eng.partition_redos())
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts, o.counts())
+    _assert_summaries_equal(got, o.snapshot(reset=True), "moving load")
+    # (level-1 redos, level-2 redos, level-2 counting first passes) after each batch
+    assert hist == [(0, 0, 1), (0, 0, 1), (0, 0, 2), (0, 0, 3)], hist
