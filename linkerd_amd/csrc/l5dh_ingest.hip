@@ -38,9 +38,11 @@ namespace {
 // and plan phase 0.138 -> 0.097 ms; C2 -0.02 ms, the smallest 8-way C3 shard -5 %
 // (profiles/r04z_ab.txt)
 constexpr uint32_t RSAMPLE = 1u << 18;
-constexpr int RS_WG = 256;              // k_rsample workgroups (<= 4096 draws each: u16 LDS counters)
+#ifndef L5DH_RS_WG
+#define L5DH_RS_WG 64
+#endif
+constexpr int RS_WG = L5DH_RS_WG;  // k_rsample workgroups (<= 65535 draws each: u16 LDS counters)
 constexpr uint32_t INVALID = 0xFFFFFFFFu;
-constexpr size_t RPLAN1_LDS = 32 * 1024 * 4;  // k_rplan1's per-tile sampled ids
 
 __device__ __forceinline__ uint32_t round_up(uint32_t x, uint32_t m) { return (x + m - 1) / m * m; }
 
@@ -107,13 +109,26 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t* lds 
   return r;
 }
 
+#ifdef L5DH_PHASES
+__device__ unsigned long long g_phase_plan[16];  // the plans: wall clock at their phase ends (thread 0)
+#define RP_MARK(k) \
+  if (threadIdx.x == 0) g_phase_plan[k] = wall_clock64();  // (k_rplan1: one workgroup)
+#define RS_MARK(k) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_phase_plan[k] = wall_clock64();
+#else
+#define RP_MARK(k)
+#define RS_MARK(k)
+#endif
+
 // ------------------------------------------------------------------------
 // Sample: key = series >> 4 = 2 tile + half.  LDS: u16 pairs of keys.
 __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ series, size_t n, uint32_t S, uint32_t K,
                                                   uint32_t* __restrict__ kest) {
   extern __shared__ uint32_t c[];  // [(K + 1) / 2]
+  RS_MARK(8)
   for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) c[i] = 0;
   __syncthreads();
+  RS_MARK(9)
   const uint64_t m = n < RSAMPLE ? n : RSAMPLE;
   const uint64_t per = (m + RS_WG - 1) / RS_WG;
   const uint64_t k0 = blockIdx.x * per, k1 = k0 + per < m ? k0 + per : m;
@@ -135,17 +150,25 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
       }
   }
   __syncthreads();
+  RS_MARK(10)
   for (uint32_t i = threadIdx.x; i < (K + 1) / 2; i += 1024) {
     const uint32_t x = c[i];
     if (x & 0xFFFFu) atomicAdd(&kest[2 * i], x & 0xFFFFu);
     if ((x >> 16) && 2 * i + 1 < K) atomicAdd(&kest[2 * i + 1], x >> 16);
   }
+  RS_MARK(11)
 }
 
 // ------------------------------------------------------------------------
-// Level-1 plan, one workgroup.  Thread j owns tiles [32 j, 32 j + 32) (F <= 32768)
-// and bin j.  Direct tiles: the <= dmax tiles with the most estimated records, at
-// least max(thr_min, 2^k), k the smallest power keeping <= dmax of them.
+// Level-1 plan, one workgroup; thread j owns direct-bitmap word j -- tiles [32 j,
+// 32 j + 32), F <= 32768 -- and bin j.  The key arrays are read coalesced (thread j
+// loads tiles 2 q, 2 q + 1 for q = j + 1024 i) and turned around through LDS, one tile
+// per word, each thread reading its 32 tiles from a rotated start (no bank
+// conflicts).  (Round 5 loaded each thread's own 32 tiles: every wave-wide 16-B load
+// touched 64 cache lines, and the loads took most of the kernel's 35 us.)  Direct
+// tiles: the <= dmax tiles with the most estimated records, at least max(thr_min,
+// 2^k), k the smallest power keeping <= dmax of them.
+constexpr size_t RPLAN1_LDS = 32768 * 4;  // one word per tile
 __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
                                                  size_t cap32, size_t dlim16, uint32_t thr_min, uint32_t dmax,
@@ -156,7 +179,7 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   __shared__ uint64_t l64[17];
   __shared__ uint32_t dl[DIRECT_MAX + 1];
   __shared__ uint32_t capl[BIN1_BINS];
-  extern __shared__ uint32_t tel[];  // [32][1024]: sampled ids of tile t0 + k at tel[k * 1024 + j]
+  extern __shared__ uint32_t tw[];  // [32768] a value per tile
   const MetaLayout L = meta_layout(F);
   const uint32_t FS = (F + ST_TILES - 1) / ST_TILES;
   const uint32_t NW = (F + 31) / 32;
@@ -164,68 +187,97 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
   const bool exact = m == n;
   const double s = m ? (double)n / (double)m : 1.0;
   const uint32_t j = threadIdx.x, t0 = j * 32;
+  const int lane = lane_id();
+  RP_MARK(0)
   if (j < 33) lh[j] = 0;
   capl[j] = 0;
-  // this thread's 32 tiles (64 consecutive key words) read once, all 16-B loads in
-  // flight together (a ragged end word by word), kept in LDS for the passes below
-  auto tile_pairs = [&](const uint32_t* __restrict__ kw, auto&& put) {
+  // both key arrays, one 16-B load per tile pair (a ragged end word by word): the
+  // estimates, then (once they are in LDS) the previous counts
+  auto load_pairs = [&](const uint32_t* __restrict__ kw, uint4 (&x)[16]) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two batches of 8 loads (bounded registers)
-      uint4 x[8];
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const uint32_t t = t0 + 2 * (8 * h + g);
-        x[g] = make_uint4(0u, 0u, 0u, 0u);
-        if (t + 1 < F) {
-          x[g] = *reinterpret_cast<const uint4*>(kw + 2 * t);
-        } else if (t < F) {
-          x[g].x = kw[2 * t];
-          x[g].y = kw[2 * t + 1];
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        put(2 * (8 * h + g), x[g].x + x[g].y);
-        put(2 * (8 * h + g) + 1, x[g].z + x[g].w);
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t t = 2u * (j + 1024u * (uint32_t)i);
+      x[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (t + 1 < F) {
+        x[i] = *reinterpret_cast<const uint4*>(kw + 2 * t);
+      } else if (t < F) {
+        x[i].x = kw[2 * t];
+        x[i].y = kw[2 * t + 1];
       }
     }
   };
-  tile_pairs(kest, [&](int k, uint32_t v) { tel[k * 1024 + j] = v; });
-  __syncthreads();
-  auto tile_est = [&](int k) -> uint32_t { return tel[k * 1024 + j]; };  // sampled ids of tile t0 + k
-  uint32_t dbits = 0;
-  for (int k = 0; k < 32; ++k) {
-    const double est = (double)tile_est(k) * s;
-    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
-    if (dmax > 0 && e >= thr_min && e > 0) atomicAdd(&lh[31 - __clz((int)e)], 1u);
+  uint2 te[16];  // tiles 2 q, 2 q + 1
+  {
+    uint4 x[16];
+    load_pairs(kest, x);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) te[i] = make_uint2(x[i].x + x[i].y, x[i].z + x[i].w);
+  }
+  auto scaled = [&](uint32_t v) -> uint32_t { return (uint32_t)fmin((double)v * s, 4294967295.0); };
+  __syncthreads();  // lh cleared
+  RP_MARK(1)
+  // log2 histogram of the estimates; a wave whose counted tiles share one bin (C2: all
+  // of them) adds once instead of 64 lanes on one LDS word
+  auto hist = [&](uint32_t v) {
+    const uint32_t e = scaled(v);
+    const bool ok = dmax > 0 && e >= thr_min && e > 0;
+    const int bin = ok ? 31 - __clz((int)e) : 0;
+    const uint64_t act = __ballot(ok);
+    if (!act) return;
+    const int b0 = __builtin_amdgcn_readlane(bin, __builtin_ctzll(act));
+    if (__ballot(ok && bin == b0) == act) {
+      if (lane == 0) atomicAdd(&lh[b0], (uint32_t)__popcll(act));
+    } else if (ok) {
+      atomicAdd(&lh[bin], 1u);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    hist(te[i].x);
+    hist(te[i].y);
   }
   __syncthreads();
-  if (j == 0) {
-    uint32_t cum = 0, thr = 0xFFFFFFFFu;
-    int kbest = 32;
-    if (dmax > 0)
-      for (int k = 31; k >= 0; --k) {
-        cum += lh[k];
-        if (cum > dmax) break;
-        kbest = k;
-      }
-    if (kbest < 32) thr = max(max(thr_min, 1u), 1u << kbest);
-    sthr = thr;
+  if (j < 64) {  // the lowest k whose tiles of >= 2^k estimated records number <= dmax
+    const uint32_t c = j < 32 ? lh[31 - j] : 0u;  // lane l: bin 31 - l
+    const uint32_t cum = wave_incl_scan32(c);     // tiles in bins >= 31 - l
+    const uint64_t ok = __ballot(dmax > 0 && j < 32 && cum <= dmax);
+    // ok is a prefix of lanes (cum only grows): its length is the number of bins taken
+    const int nb = __popcll(ok);
+    if (j == 0) sthr = nb ? max(max(thr_min, 1u), 1u << (32 - nb)) : 0xFFFFFFFFu;
   }
+  // the estimates turned around: thread j's 32 tiles from LDS
+#pragma unroll
+  for (int i = 0; i < 16; ++i) reinterpret_cast<uint2*>(tw)[j + 1024u * (uint32_t)i] = te[i];
+  uint4 xp[16];
+  load_pairs(kprev, xp);
   __syncthreads();
   const uint32_t thr = sthr;
+  RP_MARK(2)
+  uint32_t dbits = 0, E = 0;
+#pragma unroll
   for (int k = 0; k < 32; ++k) {
-    const double est = (double)tile_est(k) * s;
-    const uint32_t e = (uint32_t)fmin(est, 4294967295.0);
-    if (t0 + k < F && e >= thr) dbits |= 1u << k;
+    const uint32_t kk = (uint32_t)(k + (int)j) & 31u;
+    const uint32_t v = tw[t0 + kk];
+    if (t0 + kk < F && scaled(v) >= thr) dbits |= 1u << kk;
+    else E += v;
   }
+  __syncthreads();  // every estimate read
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    reinterpret_cast<uint2*>(tw)[j + 1024u * (uint32_t)i] = make_uint2(xp[i].x + xp[i].y, xp[i].z + xp[i].w);
+  __syncthreads();
+  uint64_t P = 0;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const uint32_t kk = (uint32_t)(k + (int)j) & 31u;
+    if (!((dbits >> kk) & 1u)) P += tw[t0 + kk];
+  }
+  RP_MARK(3)
   uint32_t cv[4] = {(uint32_t)__popc(dbits), 0u, 0u, 0u}, ct[4];
   block_excl_scan4<1024>(cv, lds4, ct);
   const uint32_t ND = ct[0];
-  if (j < 1024) {
-    meta[L.dbits() + j] = j < NW ? dbits : 0u;
-    meta[L.dpre() + j] = cv[0];
-  }
+  meta[L.dbits() + j] = j < NW ? dbits : 0u;
+  meta[L.dpre() + j] = cv[0];
   {
     uint32_t x = dbits, di = cv[0];
     while (x) {
@@ -236,23 +288,18 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
       ++di;
     }
   }
-  // super-tile bins: this thread's non-direct tiles, summed with its partner (the other
-  // half of the super-tile is lane j ^ 1 of the same wave)
-  double P = 0.0, E = 0.0;
-  tile_pairs(kprev, [&](int k, uint32_t v) {
-    if (t0 + k < F && !((dbits >> k) & 1u)) {
-      P += (double)v;
-      E += (double)tile_est(k);
-    }
-  });
+  // a super-tile's two words are lanes j, j ^ 1 of one wave
   P += __shfl_xor(P, 1, 64);
   E += __shfl_xor(E, 1, 64);
+  RP_MARK(4)
+  // super-tile bins
   if ((j & 1u) == 0 && (j >> 1) < FS) {
     const uint32_t b = j >> 1;
-    capl[b] = rcap(P, E, s, exact, 256.0, 4, pct, 6.0, true);
-    meta[L.btot() + b] = (uint32_t)fmin(P, 4294967295.0);  // the bin's previous load, for k_rfix1
+    capl[b] = rcap((double)P, (double)E, s, exact, 256.0, 4, pct, 6.0, true);
+    meta[L.btot() + b] = (uint32_t)min(P, (uint64_t)0xFFFFFFFFu);  // the bin's previous load, for k_rfix1
   }
   __syncthreads();  // dl complete
+  RP_MARK(5)
   const uint32_t TB = FS + 2 * ND;
   if (j >= FS && j < TB) {  // direct half-bins
     const uint32_t t = dl[(j - FS) >> 1], h = (j - FS) & 1u;
@@ -284,7 +331,11 @@ __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uin
     hdr[H_EXACT] = exact ? 1u : 0u;
     hdr[H_D16] = (uint32_t)min(tot16, (uint64_t)dlim16);  // level 2's regions follow the direct keys' (8-aligned)
   }
+  RP_MARK(6)
 }
+
+
+
 
 // ------------------------------------------------------------------------
 // Level 1, one 1024-thread workgroup per CU walking its slab in 16K-slot sub-chunks.
@@ -1182,6 +1233,9 @@ __global__ __launch_bounds__(256) void k_fetch_host(const uint32_t* __restrict__
 #ifdef L5DH_PHASES
 extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases3(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase3), sizeof(g_phase3), 0, hipMemcpyDeviceToHost);
+}
+extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases_plan(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_plan), sizeof(g_phase_plan), 0, hipMemcpyDeviceToHost);
 }
 extern "C" __attribute__((visibility("default"))) int l5dh_dev_phases1(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase1), sizeof(g_phase1), 0, hipMemcpyDeviceToHost);
