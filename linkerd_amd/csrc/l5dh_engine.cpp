@@ -474,12 +474,12 @@ int aggregate(l5dh_ctx* c, int final_mode, int reset, Outputs out, bool encode =
     if (split_items && big_seen) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, true, c->stream));
+      HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->side));
       HIPCHK(c, hipEventRecord(c->ev_join, c->side));
       joined = false;
     } else {
-      if (split_items) HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, false, c->stream));
+      if (split_items) HIPCHK(c, launch_accum_split(sv, pl, split_items, st, tb, out, direct_out, hc, c->stream));
       HIPCHK(c, launch_accum_cold(sv, pl, DEV_COUNT, st, tb, out, final_mode, reset, c->stream));
     }
     // (timed with the accumulate: with two streams it runs under the cold kernel)

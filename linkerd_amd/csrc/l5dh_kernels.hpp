@@ -216,7 +216,7 @@ hipError_t launch_hot_init(Plan plan, uint32_t max_hot, State state, Outputs out
 hipError_t launch_accum_cold(Segs segs, Plan plan, uint32_t cold_items, State state, Tables tb, Outputs out,
                              int final_mode, int reset, hipStream_t st);
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
-                              Outputs out, int direct_out, uint32_t hot_chunk, bool beside_cold, hipStream_t st);
+                              Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st);
 hipError_t launch_hot_finish(Plan plan, uint32_t max_hot, State state, Tables tb, Outputs out, int final_mode,
                              int reset, int direct_out, hipStream_t st);
 // Summaries of state rows [first, first+count) (ext == nullptr) or of external

@@ -1129,17 +1129,15 @@ hipError_t launch_fold1(const uint32_t* series, const float* values, size_t n, u
 }
 
 hipError_t launch_accum_split(Segs segs, Plan plan, uint32_t max_split_items, State state, Tables tb,
-                              Outputs out, int direct_out, uint32_t hot_chunk, bool beside_cold, hipStream_t st) {
+                              Outputs out, int direct_out, uint32_t hot_chunk, hipStream_t st) {
   if (max_split_items == 0) return hipSuccess;
   // at most 3/8 of the CUs: launched first, it leaves the rest to the cold tiles' kernel
   // (k_accum_split takes 115 KB of LDS: the two cannot share a CU), and its workgroups and
   // the cold ones take items until both queues are empty (accumulate phase on C3: 1.67 ms
   // with every CU first, 1.63 with half, 1.61 with 3/8; 1/4: 1.85, 5/8: 1.65;
-  // profiles/r05ab_split_fraction_ab.txt).  Alone on its stream too (`beside_cold` false:
-  // the last plan had no big tiles) -- every CU there measured the same on the split-heavy
-  // 8-way shards and cost C2 10 us for the launch of 256 idle workgroups
-  // (profiles/r06_split_grid_ab.txt).
-  (void)beside_cold;
+  // profiles/r05ab_split_fraction_ab.txt).  Alone on its stream too (the last plan had no
+  // big tiles): every CU there measured the same on the split-heavy 8-way shards and cost
+  // C2 10 us for the launch of 256 idle workgroups (profiles/r06_split_grid_ab.txt).
   const uint32_t g = std::max<uint32_t>(1u, (uint32_t)num_cus() * 3 / 8);
   hipLaunchKernelGGL(k_accum_split, dim3(std::min<uint32_t>(max_split_items, g)), dim3(WG), ACC_SPLIT_LDS, st, segs,
                      plan, state, tb, out, direct_out, hot_chunk);
