@@ -169,6 +169,10 @@ __global__ __launch_bounds__(1024) void k_rsample(const uint32_t* __restrict__ s
 // tiles: the <= dmax tiles with the most estimated records, at least max(thr_min,
 // 2^k), k the smallest power keeping <= dmax of them.
 constexpr size_t RPLAN1_LDS = 32768 * 4;  // one word per tile
+// Up to this many keys (C2, the smaller shards) the level-2 fix-up is one workgroup
+// (k_rfix2s): 6 us against 2 x 5 us on C2.  (Planning their level-2 regions in k_rplan1
+// too cost it 13 us, more than the two launches it saved: profiles/r06_plan_kernels.txt.)
+constexpr uint32_t RFIX2_ONE_WG_MAX = 16384;
 __global__ __launch_bounds__(1024) void k_rplan1(size_t n, uint32_t F, const uint32_t* __restrict__ kest,
                                                  const uint32_t* __restrict__ kprev, uint32_t* __restrict__ meta,
                                                  size_t cap32, size_t dlim16, uint32_t thr_min, uint32_t dmax,
@@ -1215,6 +1219,56 @@ __global__ __launch_bounds__(1024) void k_rfix2b(uint32_t F, uint32_t* __restric
   }
 }
 
+// k_rfix2a + k_rfix2b in one workgroup for <= RFIX2_ONE_WG_MAX keys (thread j: keys
+// [KP j, KP j + KP), in key order across threads): the exact counts to kprev, and on a
+// redo the exact regions.
+__global__ __launch_bounds__(1024) void k_rfix2s(uint32_t F, uint32_t* __restrict__ meta, uint32_t* __restrict__ kprev) {
+  __shared__ uint64_t l64[17];
+  const MetaLayout L = meta_layout(F);
+  uint32_t* hdr = meta + L.hdr();
+  constexpr uint32_t KPM = RFIX2_ONE_WG_MAX / 1024;
+  const uint32_t KP = (L.K + 1023) / 1024, k0 = threadIdx.x * KP;
+  const uint32_t redo = hdr[H_OV2] | hdr[H_COUNT2];
+  const uint32_t counted = hdr[H_COUNT2];
+  uint32_t c8[KPM], dm = 0;
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < KPM; ++q) {
+    const uint32_t k = k0 + q;
+    c8[q] = 0;
+    if (q < KP && k < L.K) {
+      const uint32_t c = meta[L.kcnt() + k];
+      kprev[k] = c;
+      if (tile_direct(meta, L, k >> 1)) {
+        dm |= 1u << q;
+      } else {
+        c8[q] = round_up(c, 8);
+        mine += c8[q];
+      }
+    }
+  }
+  __syncthreads();  // every thread has read the header
+  if (threadIdx.x == 0) hdr[H_REDO2] = redo;
+  if (!redo) return;  // (workgroup-uniform)
+  uint64_t total;
+  uint64_t kb = (uint64_t)hdr[H_D16] + block_excl_scan64(mine, l64, &total);
+#pragma unroll
+  for (uint32_t q = 0; q < KPM; ++q) {
+    const uint32_t k = k0 + q;
+    if (q < KP && k < L.K && !((dm >> q) & 1u)) {
+      meta[L.kbase() + k] = (uint32_t)kb;
+      meta[L.kcap() + k] = c8[q];
+      meta[L.kcnt() + k] = 0u;
+      kb += c8[q];
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (counted) hdr[H_NCNT2] += 1u;  // a counting first pass, not a redo
+    else hdr[H_NOVR2] += 1u;
+    hdr[H_OV2] = 0u;
+  }
+}
+
 // Small host batches into the staging ring: the GPU reads pinned host memory
 // directly (zero-copy over PCIe) -- one kernel for both arrays, instead of two
 // DMA copies whose setup dominates at 64K samples (35 us per pair measured).
@@ -1290,7 +1344,9 @@ hipError_t launch_ingest(const IngestArgs& a, int stage, hipStream_t st) {
         hipLaunchKernelGGL(k_rbin2<B2_NT>, dim3(a.num_cu * B2_PER_CU), dim3(B2_NT), 0, st, a.S, a.F, a.tb, a.meta,
                            a.meta + L.istart(), a.meta + L.bbase(), a.meta + L.btot(), a.rec32, a.rec16, a.sumfix,
                            pass);
-        if (pass == 0) {
+        if (pass == 0 && K <= RFIX2_ONE_WG_MAX) {
+          hipLaunchKernelGGL(k_rfix2s, dim3(1), dim3(1024), 0, st, a.F, a.meta, a.kprev);
+        } else if (pass == 0) {
           hipLaunchKernelGGL(k_rfix2a, dim3(B), dim3(1024), 0, st, a.F, a.meta, a.kprev);
           hipLaunchKernelGGL(k_rfix2b, dim3(B), dim3(1024), 0, st, a.F, a.meta);
         }
