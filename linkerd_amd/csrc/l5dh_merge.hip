@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void k_mpack(const uint32_t* __restrict__ src,
 // row's while this one is decoded), the first chunks of MDEC_BATCH sources with loads
 // in flight together.
 constexpr int MDEC_WAVES = 4, MDEC_BATCH = 8, MDEC_GRID = 1280;  // (5 workgroups per CU: 28.8 KB of LDS each)
+constexpr int MDEC_AHEAD = 4;
 __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint32_t nrows,
                                                              const int64_t* __restrict__ totals, Tables tb,
                                                              int32_t* __restrict__ out_rows,
@@ -120,12 +121,26 @@ __global__ __launch_bounds__(64 * MDEC_WAVES) void k_mdecode(MergeRecv src, uint
     n = ok ? src.words[ix] : 0u;
     o = ok ? src.offs[ix] : 0ull;
   };
-  auto parse = [&](uint32_t x, uint32_t nw, uint64_t off) {
+  // (a long row -- the head series hold up to 1798 words per source -- has its chunks
+  // after the first loaded MDEC_AHEAD at a time: one load latency per group of chunks,
+  // not per chunk; round 5 waited for each, which made the slice holding the head the
+  // slowest rank)
+  auto parse = [&](uint32_t x0, uint32_t nw, uint64_t off) {
     bool carry = false;  // the chunk's first word is the count of the previous chunk's last header
+    static_assert(MDEC_AHEAD == 4, "four chunk registers");
+    uint32_t xa0 = 0, xa1 = 0, xa2 = 0, xa3 = 0;  // chunks 4 g + 1 .. 4 g + 4 (no dynamic register index)
     for (uint32_t base = 0; base < nw; base += 64) {
       const uint32_t i = base + (uint32_t)lane;
       const bool valid = i < nw;
-      if (base) x = valid ? enc[off + i] : 0u;
+      const uint32_t c = base >> 6;
+      if (c % 4u == 1u) {  // chunks c .. c + 3 in flight together
+        xa0 = i < nw ? enc[off + i] : 0u;
+        xa1 = i + 64u < nw ? enc[off + i + 64u] : 0u;
+        xa2 = i + 128u < nw ? enc[off + i + 128u] : 0u;
+        xa3 = i + 192u < nw ? enc[off + i + 192u] : 0u;
+      }
+      const uint32_t k4 = (c + 3u) % 4u;  // chunk c's register (c >= 1)
+      const uint32_t x = c == 0 ? x0 : k4 == 0 ? xa0 : k4 == 1 ? xa1 : k4 == 2 ? xa2 : xa3;
       unsigned long long hm = __ballot(valid && (x & CMAX) == CMAX);  // escape headers, or counts that look like one
       unsigned long long pay = 0ull;
       if (carry) {
