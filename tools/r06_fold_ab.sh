@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 A/B of k_fold1 clearing only the LDS rows of existing series (libf1) against HEAD
+# Round-6 A/B of k_fold1 variants (libf1) against HEAD
 # (libf0): the one-tile parity tests and the C1 config test through libf1, then the C1
 # step interleaved.  Development tool.
 set -o pipefail
