@@ -529,7 +529,10 @@ int do_ingest(l5dh_ctx* c, const uint32_t* series, const float* values, size_t n
   const bool vec = ((uintptr_t)ds % 16 == 0) && ((uintptr_t)dv % 16 == 0);
   if (c->F == 1) {  // one tile: fold the batch into its state rows now (no records, no segment)
     KTimer kt(c, L5DH_K_BIN);
-    const size_t fill = n / (2 * (size_t)std::max(1, c->num_cu));  // >= 2 items per CU when the batch allows
+    // one item per CU when the batch allows (each item clears and flushes its LDS rows:
+    // C1's fold 0.040 ms at two items per CU, 0.033 at one, 0.044 at four;
+    // profiles/r06_fold_items_ab.txt)
+    const size_t fill = n / (size_t)std::max(1, c->num_cu);
     const uint32_t chunk =
         (uint32_t)std::min<size_t>(c->hot_chunk & ~3u, std::max<size_t>(16384, (fill + 1023) & ~(size_t)1023));
     HIPCHK(c, launch_fold1(ds, dv, n, chunk, state(c), tables(c), c->d_err, vec, (c->variant & 1) != 0, c->stream));
