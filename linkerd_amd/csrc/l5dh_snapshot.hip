@@ -993,7 +993,9 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
   const bool dirty = st.dirty[s >> TILE_SHIFT] != 0;
   if (dirty) {
     const SrcRow32 src{st.counts + (size_t)s * ROW};
-    const int64_t total = st.total[s];
+    // + sumfix: a one-tile space's fold leaves its escaped samples' sums there (a fold of
+    // segments into the state has moved them into `total` already: 0 then)
+    const int64_t total = st.total[s] + st.sumfix[s];
     row_pass(src, g, orow, out.words ? out.words + i : nullptr);
     if (out.summ) wave_summary(g, src, total, tb.mid, out.summ + i);
     if (totals_out && lane == 0) totals_out[i] = total;
@@ -1004,7 +1006,10 @@ __global__ __launch_bounds__(256) void k_rows(State st, const int32_t* __restric
 #pragma unroll
       for (int q = 0; q < 9; ++q)
         if (q < ng) store4_state(row, 28 * lane + 4 * q, make_uint4(0u, 0u, 0u, 0u));
-      if (lane == 0) st.total[s] = 0;
+      if (lane == 0) {
+        st.total[s] = 0;
+        st.sumfix[s] = 0;
+      }
     }
   } else {
 #pragma unroll

@@ -315,25 +315,29 @@ def test_big_tile_bins_past_u16(oracle, mode):
 
 
 @TWO_LEVEL
-def test_range_snapshot_peek_export(oracle, mode):
+@pytest.mark.parametrize("S", [500, 20], ids=["tiles", "one_tile"])
+def test_range_snapshot_peek_export(oracle, mode, S):
+    """Range snapshot (with its reset), peek, state export and summarize_dense against the
+    oracle; the one-tile space folds every batch into its state rows at ingest, escaped
+    samples' sums included (1 % edge values: negative, NaN, beyond 2^21)."""
     rng = np.random.default_rng(21)
-    S = 500
     series, vals = _random_batch(rng, S, 100_000)
     eng = _engine(S, mode)
     eng.ingest(series, vals)
     o = oracle.OracleHistograms(S)
     o.ingest(series, vals)
     want_all = o.snapshot(reset=False)
-    got = eng.snapshot(first=100, count=50, reset=True)
-    _assert_summaries_equal(got, want_all[100:150], "range")
+    a, b = (100, 150) if S > 100 else (3, 10)
+    got = eng.snapshot(first=a, count=b - a, reset=True)
+    _assert_summaries_equal(got, want_all[a:b], "range")
     # reset only that range
     got_all = eng.snapshot(reset=False)
     want_after = want_all.copy()
-    want_after[100:150] = np.zeros(50, dtype=want_after.dtype)
+    want_after[a:b] = np.zeros(b - a, dtype=want_after.dtype)
     _assert_summaries_equal(got_all, want_after, "after range reset")
     # peek == bucketAndCounts of the oracle
     L = oracle.limits()
-    for s in (0, 7, 499):
+    for s in (0, a - 1, S - 1):  # (outside the reset range)
         pk = eng.peek(s)
         c = o.counts()[s]
         nz = np.flatnonzero(c > 0)
@@ -343,10 +347,10 @@ def test_range_snapshot_peek_export(oracle, mode):
         np.testing.assert_array_equal(pk["upper"], np.where(nz < 1797, L[np.minimum(nz, 1796)], 2147483647))
     counts, totals = eng.export_state()
     want_counts = o.counts()
-    want_counts[100:150] = 0
+    want_counts[a:b] = 0
     np.testing.assert_array_equal(counts, want_counts)
     want_tot = o.totals()
-    want_tot[100:150] = 0
+    want_tot[a:b] = 0
     np.testing.assert_array_equal(totals, want_tot)
     summ = eng.summarize_dense(counts, totals)
     _assert_summaries_equal(summ, want_after, "summarize_dense")
