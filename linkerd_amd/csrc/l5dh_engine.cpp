@@ -717,7 +717,10 @@ int do_snapshot(l5dh_ctx* c, uint32_t first, uint32_t count, l5dh_summary* out, 
     }
   }
   Outputs o{d_summ, d_counts, first, count, nullptr};
-  if (full_range(c, first, count)) {
+  // (a one-tile space folds every batch into its state rows at ingest: no segments, so its
+  // snapshot is the state rows' -- one k_rows launch instead of the plan and accumulate
+  // kernels; C1 in profiles/r06_one_tile_snapshot_ab.txt)
+  if (full_range(c, first, count) && c->F > 1) {
     if ((r = aggregate(c, 1, reset, o))) return r;
   } else {
     if ((r = fold(c))) return r;
