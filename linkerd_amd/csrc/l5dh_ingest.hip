@@ -74,7 +74,11 @@ __device__ __forceinline__ uint32_t rcap(double prev, double e, double s, bool e
   } else {
     const double e0 = prev / s, sg = sqrt(e0 + 1.0);
     const double r = sqrt(e + 1.0) + 0.5 * z;
-    const double sb = ceil(r * r * s);
+    // (a level-2 key neither sampled nor seen before keeps round 5's 4 samples per draw: a
+    // sparse space has tens of thousands of them, and (1 + z / 2)^2 draws each outgrew the
+    // buffer -- a counting pass every batch, tests/test_gpu_parity.py::
+    // test_sparse_key_space_steady_state; a super-tile bin keeps its larger bound)
+    const double sb = !floor_sample && prev == 0.0 && e == 0.0 ? ceil(4.0 * s) : ceil(r * r * s);
     if (prev > 0.0 && e >= e0 - 6.0 * sg && (floor_sample || e <= e0 + 4.0 * sg)) {
       c = ceil(prev * 1.0625 + 4.0 * sqrt(prev));
       if (floor_sample) c = fmax(c, sb);

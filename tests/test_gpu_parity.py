@@ -560,3 +560,26 @@ def test_moving_load_counts_level2_first(oracle):
     _assert_summaries_equal(got, o.snapshot(reset=True), "moving load")
     # (level-1 redos, level-2 redos, level-2 counting first passes) after each batch
     assert hist == [(0, 0, 1), (0, 0, 1), (0, 0, 2), (0, 0, 3)], hist
+
+
+def test_sparse_key_space_steady_state(oracle):
+    """A sparse series space (1M series, each batch's 4M samples on 6000 of its 62.5 K
+    keys, the others never seen): after the first interval, steady batches take no redo and no
+    counting pass -- a never-sampled key's region stays small (4 samples per draw, round
+    5's bound), so the plan of ~60 K empty keys does not outgrow the buffer."""
+    rng = np.random.default_rng(77)
+    S, n = 1_000_000, 4_000_000
+    keys = rng.choice(S // 16, 6000, replace=False)  # the other ~56 K keys are never seen
+    eng = _engine(S)
+    o = oracle.OracleHistograms(S)
+    hist = []
+    for it in range(3):
+        series = (keys[rng.integers(0, keys.size, n)] * 16 + rng.integers(0, 16, n)).astype(np.uint32)
+        vals = np.exp(3 + rng.standard_normal(n)).astype(np.float32)
+        eng.ingest(series, vals)
+        o.ingest(series, vals, threads=8)
+        hist.append(eng.partition_redos())
+    got, counts = eng.snapshot(reset=True, with_counts=True)
+    np.testing.assert_array_equal(counts.sum(), 3 * n)
+    _assert_summaries_equal(got, o.snapshot(reset=True), "sparse")
+    assert hist[2][:3] == hist[0][:3], hist  # (batches 2 and 3: nothing redone or counted)
